@@ -1,0 +1,174 @@
+/*
+ * wam_hip.h -- C-ABI of libwam_hip.so, the MI355X (gfx950) kernels behind the WAM attribution path.
+ *
+ * The reference (michalpiasecki0/wam) is pure Python: its hot path calls the third-party ptwt
+ * package (not vendored; ptwt>=0.1.0, de-facto 1.0.1) for every wavelet transform and numpy for
+ * the per-subband post-processing. The entry points below replace exactly those calls; the
+ * Python classes in wam_amd/ keep the reference's class / method signatures and bind these
+ * symbols with ctypes (see INTEGRATION.md for the binding a maintainer would add).
+ *
+ * Conventions
+ *   - plain pointers + sizes only; every device buffer is allocated by the caller (torch);
+ *   - every compute entry point is asynchronous on the given hipStream_t (passed as void*);
+ *   - return value: 0 = success, otherwise a code for wam_strerror(); nothing throws;
+ *   - plans are immutable after creation and may be shared by concurrent streams;
+ *   - coefficient buffers are BAND-MAJOR: band b occupies [batch, band dims...] contiguously at
+ *     element offset batch * wam_plan_band_offset(plan, b). Band order is ptwt's:
+ *       1D: [A_J, D_J, ..., D_1]
+ *       2D: [A_J, (H_J, V_J, D_J), ..., (H_1, V_1, D_1)]   H = hi along rows, lo along columns
+ *       3D: [A_J, (aad, ada, add, daa, dad, dda, ddd)_J, ..., (...)_1]  letters = axes (-3,-2,-1)
+ */
+#ifndef WAM_HIP_H
+#define WAM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* boundary modes (ptwt names; 'constant' is ptwt's alias of torch 'replicate') */
+enum wam_mode { WAM_MODE_ZERO = 0, WAM_MODE_REFLECT = 1, WAM_MODE_SYMMETRIC = 2,
+                WAM_MODE_CONSTANT = 3, WAM_MODE_PERIODIC = 4 };
+
+/* error codes (HIP runtime errors are returned as WAM_ERR_HIP_BASE + hipError_t) */
+enum wam_status { WAM_OK = 0, WAM_ERR_INVALID_ARG = 1, WAM_ERR_SHAPE = 2, WAM_ERR_UNSUPPORTED = 3,
+                  WAM_ERR_NO_MEMORY = 4, WAM_ERR_HIP_BASE = 1000 };
+
+typedef struct wam_plan wam_plan;
+
+const char* wam_strerror(int status);
+/* library / ABI version; bumped on any signature change */
+int wam_version(void);
+
+/* ------------------------------------------------------------------------------------------------
+ * Plans: one per (ndim, spatial shape, levels, filter bank, mode). Replaces ptwt's per-call
+ * filter construction (_get_filter_tensors / _construct_{2,3}d_filt) and size bookkeeping
+ * (_get_pad, _adjust_padding_at_reconstruction).
+ * filters are pywt's float64 tables, cast to fp32 on the device (as ptwt casts to x.dtype).
+ * ---------------------------------------------------------------------------------------------- */
+int wam_plan_create(wam_plan** plan, int ndim, const int64_t* shape, int levels,
+                    const double* dec_lo, const double* dec_hi,
+                    const double* rec_lo, const double* rec_hi, int filt_len, int mode);
+/* flags: WAM_PLAN_GENERIC forces the per-axis kernels (used by tests to cross-check the fused
+ * 2D kernels); 0 selects the fastest path. wam_plan_create == wam_plan_create_ex(..., 0). */
+enum wam_plan_flags { WAM_PLAN_GENERIC = 1 };
+int wam_plan_create_ex(wam_plan** plan, int ndim, const int64_t* shape, int levels,
+                       const double* dec_lo, const double* dec_hi,
+                       const double* rec_lo, const double* rec_hi, int filt_len, int mode, int flags);
+void wam_plan_destroy(wam_plan* plan);
+int wam_plan_num_bands(const wam_plan* plan);
+/* dims of band b (ndim values) */
+int wam_plan_band_shape(const wam_plan* plan, int band, int64_t* dims);
+/* element offset of band b for ONE item (multiply by batch for a batched buffer) */
+int64_t wam_plan_band_offset(const wam_plan* plan, int band);
+/* coefficients per item (sum over bands) */
+int64_t wam_plan_coeff_numel(const wam_plan* plan);
+/* spatial dims produced by wam_waverec (ptwt: odd n reconstructs to n+1) */
+int wam_plan_rec_shape(const wam_plan* plan, int64_t* dims);
+/* bytes of scratch the transforms need for `batch` items (caller allocates) */
+int64_t wam_plan_workspace_bytes(const wam_plan* plan, int64_t batch);
+
+/* ------------------------------------------------------------------------------------------------
+ * Transforms
+ * ---------------------------------------------------------------------------------------------- */
+/* ptwt.wavedec / wavedec2 / wavedec3 (lib/wam_2D.py:96,430; lib/wam_1D.py:109,370;
+ * lib/wam_3D.py:194,620). x: [batch, shape...]; coeffs: band-major, batch items. */
+int wam_wavedec(const wam_plan* plan, int64_t batch, const float* x, float* coeffs,
+                void* workspace, void* stream);
+
+/* ptwt.waverec / waverec2 / waverec3 (lib/wam_2D.py:113; lib/wam_1D.py:117; lib/wam_3D.py:206,222)
+ * with the Integrated-Gradients path scaling fused into the coefficient load
+ * (lib/wam_2D.py:461-476 alter()): out[a, b] = waverec(fp32(alpha[a]) * coeffs[b]) for
+ * a < n_alpha; alpha is a HOST array (alpha == NULL: n_alpha must be 1, no scaling).
+ * out: [n_alpha, batch, rec_shape...]. */
+int wam_waverec(const wam_plan* plan, int64_t batch, const float* coeffs, const float* alpha,
+                int n_alpha, float* out, void* workspace, void* stream);
+
+/* Adjoint of wam_waverec w.r.t. its coefficients = the backward pass of waverec in the
+ * reference's loss.backward() (lib/wam_2D.py:116): zero-padded analysis with reverse(rec)
+ * filters. grad: [batch, rec_shape...]; coeff_grads: band-major. */
+int wam_waverec_adjoint(const wam_plan* plan, int64_t batch, const float* grad, float* coeff_grads,
+                        void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * SmoothGrad noise (lib/wam_2D.py:390-403, lib/wam_1D.py:311-322, lib/wam_3D.py:565-579)
+ * ---------------------------------------------------------------------------------------------- */
+/* sigma[i] = fp32(spread) * (max(x_i[0:len]) - min(x_i[0:len])), x_i = x + i*item_stride */
+int wam_item_sigma(int64_t items, int64_t item_stride, int64_t len, const float* x, float spread,
+                   float* sigma, void* stream);
+
+/* out[s, i, e] = x[i, e] + noise  for e < noised_len,  0 for noised_len <= e < item_stride
+ * noise = host_noise[s, i, e] if host_noise != NULL (parity mode: the numpy legacy stream), else
+ *         sigma[i] * N(0,1) from Philox4x32-10 keyed by (seed), counter (sample_base + s, i, e/4).
+ * s ranges over [0, n_samples). */
+int wam_noise_add(int64_t n_samples, int64_t items, int64_t item_stride, int64_t noised_len,
+                  const float* x, const float* sigma, const float* host_noise, uint64_t seed,
+                  int64_t sample_base, float* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Per-subband reduction and accumulation (lib/wam_2D.py:200-264 visualize_grad_wam,
+ * :268-341 _reproject_wam, :388-415 SmoothGrad mean, :441-459 IG trapezoid;
+ * lib/wam_3D.py:127-166 refactor, :585-587 legacy averaging)
+ * ---------------------------------------------------------------------------------------------- */
+/* maps[item, band-packed] = | mean over `channels` of coeff_grads |   (numpy float32 mean:
+ * ((g0 + g1) + g2 ...) / C);  band_max[group, band] = max over the group's items of maps
+ * (atomic; caller zero-fills). items = groups * group_items; coeff_grads hold items*channels
+ * signals. maps layout: item-major, bands packed with wam_plan_band_offset. */
+int wam_subband_maps(const wam_plan* plan, int64_t groups, int64_t group_items, int channels,
+                     const float* coeff_grads, float* maps, float* band_max, void* stream);
+
+/* SmoothGrad mosaic accumulation. For each group s in [0, groups) in order and item n:
+ *   frame[n, p] += fp64( maps[(s*group_items+n), src[p]] / band_max[s, band[p]] )  (normalize)
+ *   frame[n, p] += fp64( maps[...] )                                              (!normalize)
+ * src[p] = -1 leaves frame[n, p] unchanged (the reference's zero canvas). frame: [group_items,
+ * frame_len] float64. src/band: the mosaic gather map built on the host from the reference's
+ * slice-assignment rules (frame geometry lives in the Python layer). */
+int wam_frame_accumulate(int64_t groups, int64_t group_items, int64_t frame_len, const int32_t* src,
+                         const int32_t* band, const float* maps, int64_t maps_item_len,
+                         const float* band_max, int n_bands, int normalize, double* frame,
+                         void* stream);
+
+/* Integrated-Gradients mosaic + trapezoid (np.trapz(np.nan_to_num(G), axis=1), dx = 1, fp32).
+ * For step k = k0 + s, s in [0, groups):  G = nan_to_num(fp32 mosaic value (normalised));
+ *   sequential (weights == NULL): if k > 0: acc += (prev + G) / 2;  prev = G
+ *   weighted   (weights != NULL): acc += weights[s] * G     (used when steps are sharded)
+ * prev / acc: [group_items, frame_len] fp32. */
+int wam_frame_trapz(int64_t groups, int64_t k0, int64_t group_items, int64_t frame_len,
+                    const int32_t* src, const int32_t* band, const float* maps, int64_t maps_item_len,
+                    const float* band_max, int n_bands, int normalize, const float* weights,
+                    float* prev, float* acc, void* stream);
+
+/* 3D cube (lib/wam_3D.py:127-166 refactor; :585-587 legacy averaging; :638 IG trapezoid):
+ * value = maps[item, src[p]] with maps = |coeff grads| from wam_subband_maps(channels = 1)
+ * (no channel mean, no normalisation). For s in [0, groups) in order:
+ * mode 0 (legacy smooth, sequential): acc = (acc + value) / n_total                    (fp32)
+ * mode 1 (weighted):                   acc += weights[s] * value
+ * mode 2 (IG sequential trapz):        G = nan_to_num(value); if k0+s > 0: acc += (prev+G)/2;
+ *                                      prev = G
+ * acc / prev: [group_items, cube_len] fp32. */
+int wam_cube_accumulate(int64_t groups, int64_t k0, int64_t group_items, int64_t cube_len,
+                        const int32_t* src, const float* maps, int64_t maps_item_len, int mode,
+                        float n_total, const float* weights, float* prev, float* acc, void* stream);
+
+/* Sum reduction in sample order: acc[e] (+)= src[s*len + e] for s < groups (fp32, sequential);
+ * scale != 0: afterwards acc[e] = acc[e] / scale (numpy mean's true_divide). */
+int wam_accumulate_f32(int64_t groups, int64_t len, const float* src, float scale, float* acc,
+                       void* stream);
+
+/* IG trapezoid over a generic fp32 stream (1D melspec / coefficient gradients):
+ * G_s = src[s*len + e]; sequential (weights == NULL) or weighted trapz as in wam_frame_trapz;
+ * acc_f64 != NULL accumulates in fp64 (the reference's float64 path_melspecs), else acc_f32. */
+int wam_trapz_f32(int64_t groups, int64_t k0, int64_t len, const float* src, const float* weights,
+                  float* prev_f32, float* acc_f32, double* prev_f64, double* acc_f64, void* stream);
+
+/* .scales side output (lib/wam_2D.py:488-536 reproject_wam): for each item and level j,
+ * out[item, j] = sum over the H, V, D quadrants of bilinear (cv2 INTER_LINEAR, half-pixel)
+ * upsampling to size x size; with approx, out[item, J] = upsampled approximation corner. */
+int wam_reproject_scales(int64_t items, int size, int levels, int approx, const double* avg,
+                         double* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WAM_HIP_H */

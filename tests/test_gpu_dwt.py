@@ -1,0 +1,189 @@
+"""GPU parity of the HIP wavelet kernels (through the C-ABI) against the oracle / pywt fixtures.
+
+Tolerance (fp32 kernels vs float64 references): max |err| <= 2e-6 * max(|ref|, 1) per band
+(one fp32 rounding per tap; filters are fp32 casts of pywt's float64 tables, as in ptwt).
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import flat_bands, max_rel, npz, pywt_cases, pywt_coeffs
+
+pytestmark = pytest.mark.gpu
+
+TOL = 2e-6
+
+
+@pytest.fixture(scope="module")
+def wam():
+    import wam_amd
+    from wam_amd import plan
+    assert torch.cuda.is_available()
+    return plan
+
+
+def _tol(ref):
+    return TOL * max(1.0, float(np.abs(ref).max()))
+
+
+def _run_dec(P, x, dim, J, wav, mode, generic=False):
+    lead = x.shape[0]
+    shape = x.shape[1:]
+    p = P.get_plan(dim, shape, J, wav, mode, "cuda", generic=generic)
+    xt = torch.tensor(x, dtype=torch.float32, device="cuda")
+    flat = p.wavedec(xt)
+    return p, [b.cpu().numpy().astype(np.float64) for b in p.split(flat, lead)]
+
+
+@pytest.mark.parametrize("dim", [1, 2, 3])
+@pytest.mark.parametrize("generic", [False, True])
+def test_wavedec_matches_pywt(wam, dim, generic):
+    if dim != 2 and not generic:
+        pytest.skip("fused kernels are 2D")
+    d = npz("pywt_dwt.npz")
+    for case, wav, mode, J in pywt_cases(dim):
+        x = d[case + "_x"]
+        _, got = _run_dec(wam, x, dim, J, wav, mode, generic)
+        ref = flat_bands(pywt_coeffs(case, dim, J), dim)
+        assert len(got) == len(ref)
+        for b, (g, r) in enumerate(zip(got, ref)):
+            assert g.shape == r.shape, (case, b, g.shape, r.shape)
+            assert np.abs(g - r).max() <= _tol(r), (case, wav, mode, b, np.abs(g - r).max())
+
+
+@pytest.mark.parametrize("dim", [1, 2, 3])
+@pytest.mark.parametrize("generic", [False, True])
+def test_waverec_matches_pywt(wam, dim, generic):
+    """Synthesis of RANDOM coefficients (not an analysis output) vs pywt.waverec*."""
+    if dim != 2 and not generic:
+        pytest.skip("fused kernels are 2D")
+    d = npz("pywt_dwt.npz")
+    for case, wav, mode, J in pywt_cases(dim):
+        rc = flat_bands(pywt_coeffs(case, dim, J, prefix="r"), dim)
+        lead = rc[0].shape[0]
+        x = d[case + "_x"]
+        p = wam.get_plan(dim, x.shape[1:], J, wav, mode, "cuda", generic=generic)
+        flat = torch.cat([torch.tensor(b, dtype=torch.float32).reshape(-1) for b in rc]).cuda()
+        out = p.waverec(flat, lead)[0].cpu().numpy()
+        ref = d[case + "_rrec"]
+        assert out.shape == ref.shape, (case, out.shape, ref.shape)
+        assert np.abs(out - ref).max() <= _tol(ref) * 4, (case, wav, mode, np.abs(out - ref).max())
+
+
+@pytest.mark.parametrize("dim", [1, 2, 3])
+def test_adjoint_matches_oracle(wam, dim):
+    from oracle import dwt as odwt
+    rs = np.random.RandomState(5)
+    for case, wav, mode, J in pywt_cases(dim)[::3]:
+        x = npz("pywt_dwt.npz")[case + "_x"]
+        for generic in ([False, True] if dim == 2 else [True]):
+            p = wam.get_plan(dim, x.shape[1:], J, wav, mode, "cuda", generic=generic)
+            g = rs.standard_normal((x.shape[0],) + p.rec_shape)
+            got = p.adjoint(torch.tensor(g, dtype=torch.float32, device="cuda"))
+            got = [b.cpu().numpy() for b in p.split(got, x.shape[0])]
+            ref = odwt.adjointn(g, [0] * (J + 1), wav, dim)
+            ref = [ref[0]] + [lv[k] for lv in ref[1:] for k in (("da", "ad", "dd") if dim == 2 else sorted(lv))]
+            if dim == 3:
+                keys = ["aad", "ada", "add", "daa", "dad", "dda", "ddd"]
+                ref = odwt.adjointn(g, [0] * (J + 1), wav, 3)
+                ref = [ref[0]] + [lv[k] for lv in ref[1:] for k in keys]
+            for b, (gb, rb) in enumerate(zip(got, ref)):
+                assert gb.shape == rb.shape
+                assert np.abs(gb - rb).max() <= _tol(rb) * 4, (case, b, np.abs(gb - rb).max())
+
+
+@pytest.mark.parametrize("wav,shape,J", [("haar", (224, 224), 3), ("db4", (224, 224), 3), ("db4", (225, 223), 3),
+                                         ("sym8", (512, 512), 5), ("db6", (64, 96), 2)])
+def test_adjoint_dot_product(wam, wav, shape, J):
+    """<waverec(c), g> == <c, adjoint(g)> (float64 accumulation of fp32 kernel outputs)."""
+    p = wam.get_plan(2, shape, J, wav, "reflect", "cuda")
+    torch.manual_seed(0)
+    B = 3
+    c = torch.randn(B * p.coeff_numel, device="cuda")
+    g = torch.randn((B,) + p.rec_shape, device="cuda")
+    lhs = (p.waverec(c, B)[0].double() * g.double()).sum().item()
+    rhs = (c.double() * p.adjoint(g).double()).sum().item()
+    assert abs(lhs - rhs) <= 1e-5 * (abs(lhs) + c.numel() ** 0.5), (lhs, rhs)
+
+
+@pytest.mark.parametrize("wav,shape,J,B", [("db4", (224, 224), 3, 192), ("haar", (224, 224), 3, 192),
+                                           ("sym8", (512, 512), 5, 24), ("db6", (225, 131), 3, 8)])
+def test_fused_equals_generic_full_size(wam, wav, shape, J, B):
+    fused = wam.get_plan(2, shape, J, wav, "reflect", "cuda")
+    gen = wam.get_plan(2, shape, J, wav, "reflect", "cuda", generic=True)
+    torch.manual_seed(1)
+    x = torch.randn((B,) + shape, device="cuda")
+    cf, cg = fused.wavedec(x), gen.wavedec(x)
+    assert (cf - cg).abs().max().item() <= 1e-5 * cg.abs().max().item()
+    rf, rg = fused.waverec(cf, B), gen.waverec(cf, B)
+    assert (rf - rg).abs().max().item() <= 1e-5 * rg.abs().max().item()
+    g = torch.randn((B,) + fused.rec_shape, device="cuda")
+    af, ag = fused.adjoint(g), gen.adjoint(g)
+    assert (af - ag).abs().max().item() <= 1e-5 * ag.abs().max().item()
+
+
+@pytest.mark.parametrize("dim,wav,shape,J,mode", [
+    (2, "db4", (224, 224), 3, "reflect"), (2, "haar", (224, 224), 3, "reflect"),
+    (2, "sym8", (512, 512), 5, "reflect"), (2, "db4", (225, 225), 3, "symmetric"),
+    (1, "db6", (80000,), 5, "reflect"), (3, "haar", (128, 128, 128), 2, "symmetric"),
+    (3, "db4", (40, 36, 34), 2, "zero")])
+def test_roundtrip_full_size(wam, dim, wav, shape, J, mode):
+    """DWT -> IDWT round trip (reported; identity up to fp32 rounding), at BASELINE sizes."""
+    p = wam.get_plan(dim, shape, J, wav, mode, "cuda")
+    B = 4 if dim != 3 else 1
+    torch.manual_seed(2)
+    x = torch.randn((B,) + shape, device="cuda")
+    r = p.waverec(p.wavedec(x), B)[0]
+    sl = tuple(slice(0, s) for s in shape)
+    err = (r[(slice(None),) + sl] - x).abs().max().item()
+    print("roundtrip %s %s %s: max abs err %.3e" % (wav, shape, mode, err))
+    assert err <= 1e-5 * x.abs().max().item()
+
+
+def test_alpha_scaling_matches_scaled_coefficients(wam):
+    p = wam.get_plan(2, (224, 224), 3, "db4", "reflect", "cuda")
+    torch.manual_seed(3)
+    c = torch.randn(6 * p.coeff_numel, device="cuda")
+    alphas = np.linspace(0, 1, 5)
+    out = p.waverec(c, 6, alphas=alphas)
+    for i, a in enumerate(alphas):
+        ref = p.waverec(c * float(np.float32(a)), 6)[0]
+        assert torch.equal(out[i], ref)
+
+
+def test_transforms_api_autograd(wam):
+    """wam_amd.waverec2 backward == the oracle's autograd through ptwt's conv_transpose."""
+    import wam_amd
+    from oracle import ptwt_torch
+    torch.manual_seed(4)
+    x = torch.randn(2, 3, 45, 37)
+    cs = wam_amd.wavedec2(x.cuda(), "db4", level=2, mode="reflect")
+    ref_cs = ptwt_torch.wavedec2(x.double(), "db4", level=2, mode="reflect")
+    for a, b in zip(flat_bands(cs, 2), flat_bands(ref_cs, 2)):
+        assert a.shape == b.shape
+        assert (a.double().cpu() - b).abs().max().item() <= 1e-5
+    leaves = [t.detach().requires_grad_() for t in flat_bands(cs, 2)]
+    rec = wam_amd.waverec2([leaves[0]] + [wam_amd.WaveletDetailTuple2d(*leaves[1 + 3 * i:4 + 3 * i])
+                                          for i in range(2)], "db4")
+    g = torch.randn_like(rec)
+    rec.backward(g)
+    rl = [t.detach().requires_grad_() for t in flat_bands(ref_cs, 2)]
+    rr = ptwt_torch.waverec2([rl[0]] + [ptwt_torch.WaveletDetailTuple2d(*rl[1 + 3 * i:4 + 3 * i])
+                                        for i in range(2)], "db4")
+    assert rr.shape == rec.shape
+    assert (rr - rec.double().cpu()).abs().max().item() <= 1e-5
+    rr.backward(g.double().cpu())
+    for a, b in zip(leaves, rl):
+        assert (a.grad.double().cpu() - b.grad).abs().max().item() <= 1e-5
+
+
+def test_matlab_known_answers(wam):
+    """Single-level MATLAB R2012a answers (pywt test data) through the 1D kernels."""
+    d = npz("matlab_dwt.npz")
+    cases = sorted({k.rsplit("_", 1)[0] for k in d.files})
+    for c in cases:
+        mode, wav, n = c.split("_")
+        x = d[c + "_x"][None, :]
+        _, got = _run_dec(wam, x, 1, 1, wav, mode, generic=True)
+        assert max_rel(got[0][0], d[c + "_ma"]) < 1e-5, c
+        assert max_rel(got[1][0], d[c + "_md"]) < 1e-5, c

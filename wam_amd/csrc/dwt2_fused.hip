@@ -1,0 +1,315 @@
+// Fused 2D filter-bank kernels for gfx950: one level of analysis (both axes) and one level of
+// synthesis (both axes) per launch, "column-strip" layout.
+//
+// Analysis (k_dwt2_ana): one wave owns 64 output columns (one per lane) and a chunk of R output
+// rows of one plane. It walks the extended input rows top to bottom: each row segment
+// (128 + L - 2 extended columns, boundary-mapped) is staged through a wave-private LDS row with
+// coalesced dword loads, every lane filters its window horizontally (lo/hi along W, LDS reads as
+// conflict-free ds_read_b64 pairs) and pushes the two results into a register ring of the last
+// L rows; after every second row the ring is filtered vertically into LL / H / V / D. No vertical
+// halo is re-read inside a chunk and nothing but the four outputs goes back to HBM. The same
+// kernel is the adjoint (zero padding, reverse(rec) filters) used for the backward pass.
+//
+// Synthesis (k_dwt2_syn): one wave owns 64 coefficient columns and a chunk of coefficient rows.
+// Each lane keeps a ring of the last L/2 coefficient rows of A/H/V/D, combines them vertically
+// (polyphase, two output rows per coefficient row), exchanges the per-column results through a
+// wave-private LDS float4 row and combines horizontally; lanes L/2-1..63 own complete outputs, so
+// a strip produces 130 - L output columns. The IG path scaling alpha is applied on load.
+//
+// Waves are independent (no workgroup barriers): 4 waves per 256-thread block, LDS only for the
+// wave-private rows, ordered by the wave's own in-order LDS queue (wave-scope fences).
+#include "kernels.hpp"
+
+namespace {
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int L>
+__global__ void __launch_bounds__(256) k_dwt2_ana(const float* __restrict__ in, int nh, int nw, int64_t in_plane,
+                                                  float* __restrict__ oa, float* __restrict__ oh,
+                                                  float* __restrict__ ov, float* __restrict__ od, int mh, int mw,
+                                                  int64_t out_plane, int p, int mode,
+                                                  const float* __restrict__ filt, int nstrips, int nchunks, int R,
+                                                  int64_t total_waves) {
+  constexpr int SEGW = 128 + L - 2;
+  __shared__ __attribute__((aligned(16))) float seg[4][SEGW + 2];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wv;
+  if (gw >= total_waves) return;
+  const int chunk = (int)(gw % nchunks);
+  const int64_t t = gw / nchunks;
+  const int strip = (int)(t % nstrips);
+  const int64_t plane = t / nstrips;
+
+  float flo[L], fhi[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    flo[k] = filt[k];
+    fhi[k] = filt[L + k];
+  }
+  const float* src = in + plane * in_plane;
+  const int j0 = strip * 64;
+  const int j = j0 + lane;
+  const int i0 = chunk * R;
+  const int i1 = min(mh, i0 + R);
+  const int cbase = 2 * j0 - p;
+  int sc[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    int c = lane + 64 * q;
+    sc[q] = (c < SEGW) ? wam_ext_index(cbase + c, nw, mode) : -2;
+  }
+  float* myseg = seg[wv];
+
+  auto row_filter = [&](int er, float& lo, float& hi) {
+    int sr = wam_ext_index(er, nh, mode);
+    const float* row = src + (int64_t)(sr < 0 ? 0 : sr) * nw;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      if (sc[q] >= -1) {
+        float v = (sr >= 0 && sc[q] >= 0) ? row[sc[q]] : 0.f;
+        myseg[lane + 64 * q] = v;
+      }
+    }
+    wave_sync();
+    const float2* s2 = reinterpret_cast<const float2*>(myseg + 2 * lane);
+    float a = 0.f, d = 0.f;
+#pragma unroll
+    for (int k = 0; k < L; k += 2) {
+      float2 v = s2[k >> 1];
+      a = fmaf(flo[k], v.x, a);
+      d = fmaf(fhi[k], v.x, d);
+      a = fmaf(flo[k + 1], v.y, a);
+      d = fmaf(fhi[k + 1], v.y, d);
+    }
+    wave_sync();
+    lo = a;
+    hi = d;
+  };
+
+  float rl[L], rh[L];
+#pragma unroll
+  for (int k = 0; k < L - 2; ++k) row_filter(2 * i0 - p + k, rl[k], rh[k]);
+  for (int i = i0; i < i1; ++i) {
+    row_filter(2 * i - p + L - 2, rl[L - 2], rh[L - 2]);
+    row_filter(2 * i - p + L - 1, rl[L - 1], rh[L - 1]);
+    float a = 0.f, h = 0.f, v = 0.f, d = 0.f;
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      a = fmaf(flo[k], rl[k], a);
+      h = fmaf(fhi[k], rl[k], h);
+      v = fmaf(flo[k], rh[k], v);
+      d = fmaf(fhi[k], rh[k], d);
+    }
+    if (j < mw) {
+      int64_t o = plane * out_plane + (int64_t)i * mw + j;
+      oa[o] = a;
+      oh[o] = h;
+      ov[o] = v;
+      od[o] = d;
+    }
+#pragma unroll
+    for (int k = 0; k < L - 2; ++k) {
+      rl[k] = rl[k + 2];
+      rh[k] = rh[k + 2];
+    }
+  }
+}
+
+template <int L>
+__global__ void __launch_bounds__(256) k_dwt2_syn(const float* __restrict__ A, const float* __restrict__ Hh,
+                                                  const float* __restrict__ Vv, const float* __restrict__ Dd,
+                                                  int mh, int mw, float sa, float sd, float* __restrict__ out,
+                                                  int nh, int nw, int p, const float* __restrict__ filt,
+                                                  int nstrips, int nchunks, int RQ, int64_t total_waves) {
+  constexpr int H2 = L / 2;
+  constexpr int OUTQ = 65 - H2;  // coefficient columns completed per strip
+  __shared__ __attribute__((aligned(16))) float4 xch[4][64];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wv;
+  if (gw >= total_waves) return;
+  const int chunk = (int)(gw % nchunks);
+  const int64_t t = gw / nchunks;
+  const int strip = (int)(t % nstrips);
+  const int64_t plane = t / nstrips;
+
+  float rlo[L], rhi[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    rlo[k] = filt[k];
+    rhi[k] = filt[L + k];
+  }
+  const int qs = p >> 1;  // p is even (p = L - 2)
+  const int c0 = qs + strip * OUTQ - (H2 - 1);
+  const int jj = c0 + lane;
+  const bool colv = jj >= 0 && jj < mw;
+  const int64_t in_plane = (int64_t)mh * mw;
+  const float* pA = A + plane * in_plane;
+  const float* pH = Hh + plane * in_plane;
+  const float* pV = Vv + plane * in_plane;
+  const float* pD = Dd + plane * in_plane;
+  float* po = out + plane * (int64_t)nh * nw;
+  const int qlast = (p + nh - 1) >> 1;
+  const int qbeg = qs + chunk * RQ;
+  const int qend = min(qbeg + RQ, qlast + 1);
+  const bool producer = lane >= H2 - 1;
+  const int ucol = 2 * (jj - qs);  // cropped output column of r_col = 0
+
+  float ra[H2], rh_[H2], rv[H2], rd[H2];
+  auto load_row = [&](int q, float& a, float& h, float& v, float& d) {
+    if (colv && q >= 0 && q < mh) {
+      int64_t o = (int64_t)q * mw + jj;
+      a = sa * pA[o];
+      h = sd * pH[o];
+      v = sd * pV[o];
+      d = sd * pD[o];
+    } else {
+      a = h = v = d = 0.f;
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < H2 - 1; ++k) load_row(qbeg - (H2 - 1) + k, ra[k], rh_[k], rv[k], rd[k]);
+  float4* myx = xch[wv];
+  for (int q = qbeg; q < qend; ++q) {
+    load_row(q, ra[H2 - 1], rh_[H2 - 1], rv[H2 - 1], rd[H2 - 1]);
+    // vertical: rows 2q (r=0) and 2q+1 (r=1); ring index H2-1-i'' holds coefficient row q-i''
+    float lo0 = 0.f, lo1 = 0.f, hi0 = 0.f, hi1 = 0.f;
+#pragma unroll
+    for (int i2 = 0; i2 < H2; ++i2) {
+      const int s = H2 - 1 - i2;
+      lo0 = fmaf(rlo[2 * i2], ra[s], lo0);
+      lo0 = fmaf(rhi[2 * i2], rh_[s], lo0);
+      lo1 = fmaf(rlo[2 * i2 + 1], ra[s], lo1);
+      lo1 = fmaf(rhi[2 * i2 + 1], rh_[s], lo1);
+      hi0 = fmaf(rlo[2 * i2], rv[s], hi0);
+      hi0 = fmaf(rhi[2 * i2], rd[s], hi0);
+      hi1 = fmaf(rlo[2 * i2 + 1], rv[s], hi1);
+      hi1 = fmaf(rhi[2 * i2 + 1], rd[s], hi1);
+    }
+    myx[lane] = make_float4(lo0, lo1, hi0, hi1);
+    wave_sync();
+    if (producer) {
+      float o00 = 0.f, o01 = 0.f, o10 = 0.f, o11 = 0.f;  // o[row r][col c]
+#pragma unroll
+      for (int i2 = 0; i2 < H2; ++i2) {
+        float4 n = myx[lane - i2];
+        o00 = fmaf(rlo[2 * i2], n.x, o00);
+        o00 = fmaf(rhi[2 * i2], n.z, o00);
+        o01 = fmaf(rlo[2 * i2 + 1], n.x, o01);
+        o01 = fmaf(rhi[2 * i2 + 1], n.z, o01);
+        o10 = fmaf(rlo[2 * i2], n.y, o10);
+        o10 = fmaf(rhi[2 * i2], n.w, o10);
+        o11 = fmaf(rlo[2 * i2 + 1], n.y, o11);
+        o11 = fmaf(rhi[2 * i2 + 1], n.w, o11);
+      }
+      const int r0 = 2 * (q - qs);  // cropped output row of r = 0
+      if (ucol >= 0) {
+        if (r0 < nh) {
+          if (ucol < nw) po[(int64_t)r0 * nw + ucol] = o00;
+          if (ucol + 1 < nw) po[(int64_t)r0 * nw + ucol + 1] = o01;
+        }
+        if (r0 + 1 < nh) {
+          if (ucol < nw) po[(int64_t)(r0 + 1) * nw + ucol] = o10;
+          if (ucol + 1 < nw) po[(int64_t)(r0 + 1) * nw + ucol + 1] = o11;
+        }
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < H2 - 1; ++k) {
+      ra[k] = ra[k + 1];
+      rh_[k] = rh_[k + 1];
+      rv[k] = rv[k + 1];
+      rd[k] = rd[k + 1];
+    }
+  }
+}
+
+constexpr int kTargetWaves = 16384;
+
+template <int L>
+int launch_ana_L(int64_t batch, const float* in, int nh, int nw, int mh, int mw, int mode, const float* filt, float* oa,
+                 float* oh, float* ov, float* od, int p, hipStream_t st) {
+  int nstrips = (mw + 63) / 64;
+  int64_t base = batch * nstrips;
+  int64_t want = (kTargetWaves + base - 1) / base;
+  int maxchunks = (mh + 7) / 8;
+  int nchunks = (int)(want < 1 ? 1 : (want > maxchunks ? maxchunks : want));
+  if (nchunks < 1) nchunks = 1;
+  int R = (mh + nchunks - 1) / nchunks;
+  nchunks = (mh + R - 1) / R;
+  int64_t waves = base * nchunks;
+  int64_t blocks = (waves + 3) / 4;
+  hipLaunchKernelGGL(k_dwt2_ana<L>, dim3((unsigned)blocks), dim3(256), 0, st, in, nh, nw, (int64_t)nh * nw, oa, oh, ov,
+                     od, mh, mw, (int64_t)mh * mw, p, mode, filt, nstrips, nchunks, R, waves);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+template <int L>
+int launch_syn_L(int64_t batch, const float* A, const float* H, const float* V, const float* D, int mh, int mw, float sa,
+                 float sd, float* out, int nh, int nw, int p, const float* filt, hipStream_t st) {
+  constexpr int OUTQ = 65 - L / 2;
+  int qcols = (nw + 1) / 2;
+  int nstrips = (qcols + OUTQ - 1) / OUTQ;
+  int nq = (nh + 1) / 2;
+  int64_t base = batch * nstrips;
+  int64_t want = (kTargetWaves + base - 1) / base;
+  int maxchunks = (nq + 3) / 4;
+  int nchunks = (int)(want < 1 ? 1 : (want > maxchunks ? maxchunks : want));
+  if (nchunks < 1) nchunks = 1;
+  int RQ = (nq + nchunks - 1) / nchunks;
+  nchunks = (nq + RQ - 1) / RQ;
+  int64_t waves = base * nchunks;
+  int64_t blocks = (waves + 3) / 4;
+  hipLaunchKernelGGL(k_dwt2_syn<L>, dim3((unsigned)blocks), dim3(256), 0, st, A, H, V, D, mh, mw, sa, sd, out, nh, nw,
+                     p, filt, nstrips, nchunks, RQ, waves);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+}  // namespace
+
+bool dwt2_fused_supported(const wam_plan* p) {
+  return p->ndim == 2 && p->L <= 20 && !(p->L & 1) && (p->shape[0] < (1 << 30)) && (p->shape[1] < (1 << 30));
+}
+
+int launch_dwt2_analysis_fused(const wam_plan* p, int64_t batch, const float* in, const int64_t* in_dims,
+                               const int64_t* out_dims, int mode, int fset, float* out_a, float* const* sub,
+                               hipStream_t st) {
+  const float* filt = p->d_filt + fset * p->L;  // fset, fset+1 are adjacent (lo then hi)
+  int nh = (int)in_dims[0], nw = (int)in_dims[1], mh = (int)out_dims[0], mw = (int)out_dims[1];
+  // sub order (ptwt): 0 = H ('da': hi along rows), 1 = V ('ad'), 2 = D
+  float *oa = out_a, *oh = sub[0], *ov = sub[1], *od = sub[2];
+#define WAM_ANA_CASE(LL) \
+  case LL: return launch_ana_L<LL>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, p->pad, st);
+  switch (p->L) {
+    WAM_ANA_CASE(2) WAM_ANA_CASE(4) WAM_ANA_CASE(6) WAM_ANA_CASE(8) WAM_ANA_CASE(10)
+    WAM_ANA_CASE(12) WAM_ANA_CASE(14) WAM_ANA_CASE(16) WAM_ANA_CASE(18) WAM_ANA_CASE(20)
+    default: return WAM_ERR_UNSUPPORTED;
+  }
+#undef WAM_ANA_CASE
+}
+
+int launch_dwt2_synthesis_fused(const wam_plan* p, int64_t batch, int level, const float* a_in, float a_scale,
+                                const float* const* sub, float d_scale, float* out, hipStream_t st) {
+  const float* filt = p->d_filt + WAM_F_SYN_LO * p->L;
+  int mh = (int)p->lout[level][0], mw = (int)p->lout[level][1];
+  int nh = (int)(2 * mh - 2 + p->L - 2 * p->pad - p->extra[level][0]);
+  int nw = (int)(2 * mw - 2 + p->L - 2 * p->pad - p->extra[level][1]);
+#define WAM_SYN_CASE(LL)                                                                                       \
+  case LL: return launch_syn_L<LL>(batch, a_in, sub[0], sub[1], sub[2], mh, mw, a_scale, d_scale, out, nh, nw, \
+                                   p->pad, filt, st);
+  switch (p->L) {
+    WAM_SYN_CASE(2) WAM_SYN_CASE(4) WAM_SYN_CASE(6) WAM_SYN_CASE(8) WAM_SYN_CASE(10)
+    WAM_SYN_CASE(12) WAM_SYN_CASE(14) WAM_SYN_CASE(16) WAM_SYN_CASE(18) WAM_SYN_CASE(20)
+    default: return WAM_ERR_UNSUPPORTED;
+  }
+#undef WAM_SYN_CASE
+}

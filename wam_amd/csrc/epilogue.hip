@@ -1,0 +1,470 @@
+// WAM-specific kernels around the transforms: SmoothGrad noise, per-subband channel-mean |.| with
+// batch-global maxima, mosaic / cube accumulation (SmoothGrad mean, IG trapezoid, legacy 3D
+// averaging), generic sample accumulators and the .scales reprojection.
+// Reference: lib/wam_2D.py:200-264 (visualize_grad_wam), :268-341 (_reproject_wam),
+// :379-415 (smooth_gradcam), :417-459 (intergrated_wam), :488-536 (reproject_wam);
+// lib/wam_1D.py:294-343, :353-421; lib/wam_3D.py:127-166, :550-591, :614-643.
+#include <math.h>
+
+#include "kernels.hpp"
+
+namespace {
+
+// ------------------------------------------------------------------------------ wave reductions
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// numpy-compatible max: NaN propagates (fmaxf would drop it)
+__device__ __forceinline__ float nan_max(float a, float b) { return (a != a || a > b) ? a : b; }
+
+// ------------------------------------------------------------------------------ sigma
+__global__ void __launch_bounds__(256) k_item_sigma(const float* __restrict__ x, int64_t item_stride, int64_t len,
+                                                    float spread, float* __restrict__ sigma) {
+  const float* xi = x + blockIdx.x * item_stride;
+  float mx = -INFINITY, mn = INFINITY;
+  for (int64_t e = threadIdx.x; e < len; e += blockDim.x) {
+    float v = xi[e];
+    mx = fmaxf(mx, v);
+    mn = fminf(mn, v);
+  }
+  mx = wave_max(mx);
+  mn = wave_min(mn);
+  __shared__ float smx[4], smn[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    smx[wv] = mx;
+    smn[wv] = mn;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+      mx = fmaxf(mx, smx[w]);
+      mn = fminf(mn, smn[w]);
+    }
+    // torch: spread * (max - min) in fp32 with the python scalar cast to fp32
+    sigma[blockIdx.x] = spread * (mx - mn);
+  }
+}
+
+// ------------------------------------------------------------------------------ Philox noise
+struct u4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    c = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
+  const float two32inv = 2.3283064365386963e-10f;  // 2^-32
+  float u1 = ((float)a + 1.0f) * two32inv;         // (0, 1]
+  float u2 = (float)b * two32inv;                  // [0, 1)
+  float r = sqrtf(-2.0f * logf(u1));
+  float s, c;
+  sincospif(2.0f * u2, &s, &c);
+  z0 = r * c;
+  z1 = r * s;
+}
+
+__global__ void __launch_bounds__(256) k_noise_add(int64_t n_samples, int64_t items, int64_t item_stride,
+                                                   int64_t noised_len, const float* __restrict__ x,
+                                                   const float* __restrict__ sigma,
+                                                   const float* __restrict__ host_noise, uint32_t k0, uint32_t k1,
+                                                   int64_t sample_base, float* __restrict__ out) {
+  const int64_t groups = (item_stride + 3) / 4;
+  const int64_t total = n_samples * items * groups;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t g = t % groups;
+    int64_t q = t / groups;
+    int64_t i = q % items;
+    int64_t s = q / items;
+    float z[4] = {0.f, 0.f, 0.f, 0.f};
+    if (!host_noise && 4 * g < noised_len) {
+      u4 c = {(uint32_t)g, (uint32_t)(g >> 32) ^ ((uint32_t)i << 8), (uint32_t)(sample_base + s), (uint32_t)i};
+      u4 r = philox4x32_10(c, k0, k1);
+      box_muller(r.x, r.y, z[0], z[1]);
+      box_muller(r.z, r.w, z[2], z[3]);
+    }
+    const float sg = host_noise ? 0.f : sigma[i];
+    const float* xi = x + i * item_stride;
+    float* oi = out + (s * items + i) * item_stride;
+    const float* hn = host_noise ? host_noise + (s * items + i) * item_stride : nullptr;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      int64_t e = 4 * g + u;
+      if (e >= item_stride) break;
+      float v;
+      if (e < noised_len) v = xi[e] + (hn ? hn[e] : sg * z[u]);
+      else v = 0.f;
+      oi[e] = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ subband maps
+struct BandTable {
+  int64_t off[WAM_MAX_BANDS + 1];  // per-item packed offsets
+  int nbands;
+};
+
+// grid: x = chunk of the band, y = band, z = item. One atomic max per block and band.
+__global__ void __launch_bounds__(256) k_subband_maps(BandTable bt, int64_t items_total, int64_t group_items,
+                                                      int channels, const float* __restrict__ g,
+                                                      float* __restrict__ maps, float* __restrict__ band_max) {
+  const int b = blockIdx.y;
+  const int64_t item = blockIdx.z;
+  const int64_t nb = bt.off[b + 1] - bt.off[b];
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((int64_t)blockIdx.x * blockDim.x >= nb) return;  // whole block idle
+  float v = 0.f;
+  const bool valid = q < nb;
+  if (valid) {
+    // band-major coefficient grads: band b holds [items_total * channels, nb]
+    const float* base = g + items_total * channels * bt.off[b] + (item * channels) * nb + q;
+    float acc = base[0];
+    for (int c = 1; c < channels; ++c) acc = acc + base[(int64_t)c * nb];
+    acc = acc / (float)channels;  // numpy mean: sum then true_divide
+    v = fabsf(acc);
+    maps[item * bt.off[bt.nbands] + bt.off[b] + q] = v;
+  }
+  float m = valid ? v : 0.f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = nan_max(m, __shfl_xor(m, o, 64));
+  __shared__ float sm[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) sm[wv] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) m = nan_max(m, sm[w]);
+    const int64_t grp = item / group_items;
+    // non-negative floats order like their bit patterns; NaN (0x7fc00000) wins like numpy's max
+    atomicMax(reinterpret_cast<unsigned int*>(band_max + grp * bt.nbands + b), __float_as_uint(m));
+  }
+}
+
+// ------------------------------------------------------------------------------ frame accumulate
+__global__ void __launch_bounds__(256) k_frame_accumulate(int64_t groups, int64_t group_items, int64_t frame_len,
+                                                          const int32_t* __restrict__ src,
+                                                          const int32_t* __restrict__ band,
+                                                          const float* __restrict__ maps, int64_t maps_item_len,
+                                                          const float* __restrict__ band_max, int n_bands,
+                                                          int normalize, double* __restrict__ frame) {
+  const int64_t total = group_items * frame_len;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = t % frame_len;
+    const int64_t n = t / frame_len;
+    const int32_t sidx = src[p];
+    if (sidx < 0) continue;
+    const int32_t b = band[p];
+    double acc = frame[t];
+    for (int64_t s = 0; s < groups; ++s) {
+      float v = maps[(s * group_items + n) * maps_item_len + sidx];
+      if (normalize) v = v / band_max[s * n_bands + b];
+      acc += (double)v;
+    }
+    frame[t] = acc;
+  }
+}
+
+__device__ __forceinline__ float nan_to_num(float v) {
+  if (v != v) return 0.f;
+  if (isinf(v)) return v > 0 ? 3.4028234663852886e+38f : -3.4028234663852886e+38f;
+  return v;
+}
+
+__global__ void __launch_bounds__(256) k_frame_trapz(int64_t groups, int64_t k0, int64_t group_items, int64_t frame_len,
+                                                     const int32_t* __restrict__ src, const int32_t* __restrict__ band,
+                                                     const float* __restrict__ maps, int64_t maps_item_len,
+                                                     const float* __restrict__ band_max, int n_bands, int normalize,
+                                                     const float* __restrict__ weights, float* __restrict__ prev,
+                                                     float* __restrict__ acc) {
+  const int64_t total = group_items * frame_len;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = t % frame_len;
+    const int64_t n = t / frame_len;
+    const int32_t sidx = src[p];
+    const int32_t b = band[p];
+    float a = acc[t];
+    float pv = prev[t];
+    for (int64_t s = 0; s < groups; ++s) {
+      float v = 0.f;
+      if (sidx >= 0) {
+        v = maps[(s * group_items + n) * maps_item_len + sidx];
+        if (normalize) v = v / band_max[s * n_bands + b];
+      }
+      v = nan_to_num(v);
+      if (weights) {
+        a = fmaf(weights[s], v, a);
+      } else {
+        if (k0 + s > 0) a = a + (pv + v) / 2.0f;
+        pv = v;
+      }
+    }
+    acc[t] = a;
+    prev[t] = pv;
+  }
+}
+
+// cube: value = |g| from item-major maps (channels = 1); see wam_cube_accumulate
+__global__ void __launch_bounds__(256) k_cube_accumulate(int64_t groups, int64_t k0, int64_t group_items,
+                                                         int64_t cube_len, const int32_t* __restrict__ src,
+                                                         const float* __restrict__ maps, int64_t maps_item_len, int mode,
+                                                         float n_total, const float* __restrict__ weights,
+                                                         float* __restrict__ prev, float* __restrict__ acc) {
+  const int64_t total = group_items * cube_len;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = t % cube_len;
+    const int64_t n = t / cube_len;
+    const int32_t sidx = src[p];
+    float a = acc[t];
+    float pv = prev ? prev[t] : 0.f;
+    for (int64_t s = 0; s < groups; ++s) {
+      float v = sidx >= 0 ? maps[(s * group_items + n) * maps_item_len + sidx] : 0.f;
+      if (mode == 0) {
+        a = (a + v) / n_total;
+      } else if (mode == 1) {
+        a = fmaf(weights[s], v, a);
+      } else {
+        v = nan_to_num(v);
+        if (k0 + s > 0) a = a + (pv + v) / 2.0f;
+        pv = v;
+      }
+    }
+    acc[t] = a;
+    if (prev) prev[t] = pv;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_accumulate_f32(int64_t groups, int64_t len, const float* __restrict__ src,
+                                                        float scale, float* __restrict__ acc) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < len; e += (int64_t)gridDim.x * blockDim.x) {
+    float a = acc[e];
+    for (int64_t s = 0; s < groups; ++s) a = a + src[s * len + e];
+    if (scale != 0.f) a = a / scale;
+    acc[e] = a;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_trapz_f32(int64_t groups, int64_t k0, int64_t len, const float* __restrict__ src,
+                                                   const float* __restrict__ weights, float* __restrict__ prev32,
+                                                   float* __restrict__ acc32, double* __restrict__ prev64,
+                                                   double* __restrict__ acc64) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < len; e += (int64_t)gridDim.x * blockDim.x) {
+    if (acc64) {
+      double a = acc64[e], pv = prev64 ? prev64[e] : 0.0;
+      for (int64_t s = 0; s < groups; ++s) {
+        double v = (double)src[s * len + e];
+        if (weights) {
+          a = fma((double)weights[s], v, a);
+        } else {
+          if (k0 + s > 0) a = a + (pv + v) / 2.0;
+          pv = v;
+        }
+      }
+      acc64[e] = a;
+      if (prev64) prev64[e] = pv;
+    } else {
+      float a = acc32[e], pv = prev32 ? prev32[e] : 0.f;
+      for (int64_t s = 0; s < groups; ++s) {
+        float v = src[s * len + e];
+        if (weights) {
+          a = fmaf(weights[s], v, a);
+        } else {
+          if (k0 + s > 0) a = a + (pv + v) / 2.0f;
+          pv = v;
+        }
+      }
+      acc32[e] = a;
+      if (prev32) prev32[e] = pv;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ .scales
+// cv2.resize INTER_LINEAR (upsampling): src = (dst + 0.5) * (in / out) - 0.5, clamped to the edge.
+__device__ __forceinline__ double bilinear(const double* __restrict__ img, int ld, int ih, int iw, int oy, int ox,
+                                           int out) {
+  double sy = ((double)oy + 0.5) * ((double)ih / out) - 0.5;
+  double sx = ((double)ox + 0.5) * ((double)iw / out) - 0.5;
+  if (sy < 0) sy = 0;
+  if (sx < 0) sx = 0;
+  int y0 = (int)sy, x0 = (int)sx;
+  if (y0 > ih - 1) y0 = ih - 1;
+  if (x0 > iw - 1) x0 = iw - 1;
+  int y1 = y0 + (y0 < ih - 1 ? 1 : 0), x1 = x0 + (x0 < iw - 1 ? 1 : 0);
+  double fy = sy - y0, fx = sx - x0;
+  if (fy > 1) fy = 1;
+  if (fx > 1) fx = 1;
+  double v00 = img[(int64_t)y0 * ld + x0], v01 = img[(int64_t)y0 * ld + x1];
+  double v10 = img[(int64_t)y1 * ld + x0], v11 = img[(int64_t)y1 * ld + x1];
+  return (1 - fy) * ((1 - fx) * v00 + fx * v01) + fy * ((1 - fx) * v10 + fx * v11);
+}
+
+__global__ void __launch_bounds__(256) k_reproject(int64_t items, int size, int levels, int approx,
+                                                   const double* __restrict__ avg, double* __restrict__ out) {
+  const int nl = levels + (approx ? 1 : 0);
+  const int64_t plane = (int64_t)size * size;
+  const int64_t total = items * nl * plane;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t pix = t % plane;
+    int64_t q = t / plane;
+    int j = (int)(q % nl);
+    int64_t it = q / nl;
+    int oy = (int)(pix / size), ox = (int)(pix % size);
+    const double* a = avg + it * plane;
+    double v;
+    if (j < levels) {
+      int e = (int)(size / (double)(1 << j));
+      int s = (int)(size / (double)(1 << (j + 1)));
+      int n = e - s;
+      // horizontal = avg[:s, s:e], vertical = avg[s:e, :s], diagonal = avg[s:e, s:e]
+      v = bilinear(a + s, size, s, n, oy, ox, size) + bilinear(a + (int64_t)s * size, size, n, s, oy, ox, size) +
+          bilinear(a + (int64_t)s * size + s, size, n, n, oy, ox, size);
+    } else {
+      int e = (int)(size / (double)(1 << levels));
+      v = bilinear(a, size, e, e, oy, ox, size);
+    }
+    out[t] = v;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int wam_item_sigma(int64_t items, int64_t item_stride, int64_t len, const float* x, float spread, float* sigma,
+                   void* stream) {
+  if (items < 0 || len < 1 || !x || !sigma) return WAM_ERR_INVALID_ARG;
+  if (items == 0) return WAM_OK;
+  hipLaunchKernelGGL(k_item_sigma, dim3((unsigned)items), dim3(256), 0, (hipStream_t)stream, x, item_stride, len, spread,
+                     sigma);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int wam_noise_add(int64_t n_samples, int64_t items, int64_t item_stride, int64_t noised_len, const float* x,
+                  const float* sigma, const float* host_noise, uint64_t seed, int64_t sample_base, float* out,
+                  void* stream) {
+  if (n_samples < 0 || items < 0 || item_stride < 1 || noised_len < 0 || noised_len > item_stride || !x || !out)
+    return WAM_ERR_INVALID_ARG;
+  if (!host_noise && !sigma) return WAM_ERR_INVALID_ARG;
+  int64_t work = n_samples * items * ((item_stride + 3) / 4);
+  if (work == 0) return WAM_OK;
+  hipLaunchKernelGGL(k_noise_add, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, n_samples, items,
+                     item_stride, noised_len, x, sigma, host_noise, (uint32_t)seed, (uint32_t)(seed >> 32),
+                     sample_base, out);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int wam_subband_maps(const wam_plan* p, int64_t groups, int64_t group_items, int channels, const float* coeff_grads,
+                     float* maps, float* band_max, void* stream) {
+  if (!p || groups < 0 || group_items < 0 || channels < 1 || !coeff_grads || !maps || !band_max)
+    return WAM_ERR_INVALID_ARG;
+  int64_t items = groups * group_items;
+  if (items == 0) return WAM_OK;
+  if (items > 65535) return WAM_ERR_UNSUPPORTED;
+  BandTable bt;
+  bt.nbands = p->nbands;
+  int64_t maxb = 0;
+  for (int b = 0; b <= p->nbands; ++b) bt.off[b] = p->band_off[b];
+  for (int b = 0; b < p->nbands; ++b) maxb = std::max(maxb, p->band_off[b + 1] - p->band_off[b]);
+  dim3 grid((unsigned)((maxb + 255) / 256), (unsigned)p->nbands, (unsigned)items);
+  hipLaunchKernelGGL(k_subband_maps, grid, dim3(256), 0, (hipStream_t)stream, bt, items, group_items, channels,
+                     coeff_grads, maps, band_max);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int wam_frame_accumulate(int64_t groups, int64_t group_items, int64_t frame_len, const int32_t* src,
+                         const int32_t* band, const float* maps, int64_t maps_item_len, const float* band_max,
+                         int n_bands, int normalize, double* frame, void* stream) {
+  if (groups < 0 || group_items < 0 || frame_len < 0 || !src || !band || !maps || !frame) return WAM_ERR_INVALID_ARG;
+  if (normalize && !band_max) return WAM_ERR_INVALID_ARG;
+  int64_t work = group_items * frame_len;
+  if (work == 0 || groups == 0) return WAM_OK;
+  hipLaunchKernelGGL(k_frame_accumulate, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, groups,
+                     group_items, frame_len, src, band, maps, maps_item_len, band_max, n_bands, normalize, frame);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int wam_frame_trapz(int64_t groups, int64_t k0, int64_t group_items, int64_t frame_len, const int32_t* src,
+                    const int32_t* band, const float* maps, int64_t maps_item_len, const float* band_max, int n_bands,
+                    int normalize, const float* weights, float* prev, float* acc, void* stream) {
+  if (groups < 0 || group_items < 0 || frame_len < 0 || !src || !band || !maps || !prev || !acc)
+    return WAM_ERR_INVALID_ARG;
+  if (normalize && !band_max) return WAM_ERR_INVALID_ARG;
+  int64_t work = group_items * frame_len;
+  if (work == 0 || groups == 0) return WAM_OK;
+  hipLaunchKernelGGL(k_frame_trapz, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, groups, k0,
+                     group_items, frame_len, src, band, maps, maps_item_len, band_max, n_bands, normalize, weights,
+                     prev, acc);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int wam_cube_accumulate(int64_t groups, int64_t k0, int64_t group_items, int64_t cube_len, const int32_t* src,
+                        const float* maps, int64_t maps_item_len, int mode, float n_total, const float* weights,
+                        float* prev, float* acc, void* stream) {
+  if (groups < 0 || group_items < 0 || cube_len < 0 || !src || !maps || !acc || mode < 0 || mode > 2)
+    return WAM_ERR_INVALID_ARG;
+  if ((mode == 1 && !weights) || (mode == 2 && !prev)) return WAM_ERR_INVALID_ARG;
+  int64_t work = group_items * cube_len;
+  if (work == 0 || groups == 0) return WAM_OK;
+  hipLaunchKernelGGL(k_cube_accumulate, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, groups, k0,
+                     group_items, cube_len, src, maps, maps_item_len, mode, n_total, weights, prev, acc);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int wam_accumulate_f32(int64_t groups, int64_t len, const float* src, float scale, float* acc, void* stream) {
+  if (groups < 0 || len < 0 || !src || !acc) return WAM_ERR_INVALID_ARG;
+  if (len == 0) return WAM_OK;
+  hipLaunchKernelGGL(k_accumulate_f32, dim3(wam_grid(len, 256)), dim3(256), 0, (hipStream_t)stream, groups, len, src,
+                     scale, acc);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int wam_trapz_f32(int64_t groups, int64_t k0, int64_t len, const float* src, const float* weights, float* prev_f32,
+                  float* acc_f32, double* prev_f64, double* acc_f64, void* stream) {
+  if (groups < 0 || len < 0 || !src) return WAM_ERR_INVALID_ARG;
+  if (!acc_f64 && !acc_f32) return WAM_ERR_INVALID_ARG;
+  if (!weights && !(acc_f64 ? (void*)prev_f64 : (void*)prev_f32)) return WAM_ERR_INVALID_ARG;
+  if (len == 0 || groups == 0) return WAM_OK;
+  hipLaunchKernelGGL(k_trapz_f32, dim3(wam_grid(len, 256)), dim3(256), 0, (hipStream_t)stream, groups, k0, len, src,
+                     weights, prev_f32, acc_f32, prev_f64, acc_f64);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int wam_reproject_scales(int64_t items, int size, int levels, int approx, const double* avg, double* out,
+                         void* stream) {
+  if (items < 0 || size < 1 || levels < 1 || !avg || !out) return WAM_ERR_INVALID_ARG;
+  int64_t work = items * (levels + (approx ? 1 : 0)) * (int64_t)size * size;
+  if (work == 0) return WAM_OK;
+  hipLaunchKernelGGL(k_reproject, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, items, size, levels,
+                     approx, avg, out);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+}  // extern "C"

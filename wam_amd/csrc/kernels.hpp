@@ -1,0 +1,18 @@
+// Internal launch interfaces shared between the translation units of libwam_hip.so.
+#pragma once
+#include "common.hpp"
+
+// generic per-axis kernels (dwt_axis.hip)
+int launch_analysis_axis(const float* in, float* lo, float* hi, int64_t outer, int n, int m, int64_t inner,
+                         int padl, int mode, const float* flo, const float* fhi, int L, hipStream_t st);
+int launch_synthesis_axis(const float* a, const float* d, float* out, int64_t outer, int m, int nout,
+                          int64_t inner, int p, const float* rlo, const float* rhi, int L, float sa, float sd,
+                          hipStream_t st);
+
+// fused 2D kernels (dwt2_fused.hip)
+bool dwt2_fused_supported(const wam_plan* p);
+int launch_dwt2_analysis_fused(const wam_plan* p, int64_t batch, const float* in, const int64_t* in_dims,
+                               const int64_t* out_dims, int mode, int fset, float* out_a, float* const* sub,
+                               hipStream_t st);
+int launch_dwt2_synthesis_fused(const wam_plan* p, int64_t batch, int level, const float* a_in, float a_scale,
+                                const float* const* sub, float d_scale, float* out, hipStream_t st);

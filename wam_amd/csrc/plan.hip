@@ -1,0 +1,417 @@
+// Plans, size bookkeeping and the multi-level transform drivers of libwam_hip.so.
+//
+// Semantics (restated from ptwt, the reference's wavelet dependency):
+//   analysis per axis: p = (2L-3)//2, pad (p, p + n%2), m = (n + 2p + n%2 - L)//2 + 1
+//   synthesis per axis: conv_transpose stride 2 (length 2m-2+L), crop p at both ends, plus one
+//   more at the end when the next finer coefficient is one shorter (ptwt
+//   _adjust_padding_at_reconstruction)
+//   adjoint of synthesis = zero-padded analysis with reverse(rec) filters.
+// 2D transforms run on the fused LDS kernels in dwt2_fused.hip; 1D / 3D (and 2D with filters
+// longer than the fused kernels support) run on the generic per-axis kernels in dwt_axis.hip.
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "common.hpp"
+#include "kernels.hpp"
+
+extern "C" {
+
+int wam_version(void) { return 1; }
+
+const char* wam_strerror(int status) {
+  switch (status) {
+    case WAM_OK: return "success";
+    case WAM_ERR_INVALID_ARG: return "wam: invalid argument";
+    case WAM_ERR_SHAPE: return "wam: shape error (coefficient sizes do not match the plan)";
+    case WAM_ERR_UNSUPPORTED: return "wam: unsupported configuration";
+    case WAM_ERR_NO_MEMORY: return "wam: out of memory";
+    default: break;
+  }
+  if (status >= WAM_ERR_HIP_BASE) return hipGetErrorString((hipError_t)(status - WAM_ERR_HIP_BASE));
+  return "wam: unknown error";
+}
+
+int wam_plan_create(wam_plan** out, int ndim, const int64_t* shape, int levels, const double* dec_lo,
+                    const double* dec_hi, const double* rec_lo, const double* rec_hi, int L, int mode) {
+  return wam_plan_create_ex(out, ndim, shape, levels, dec_lo, dec_hi, rec_lo, rec_hi, L, mode, 0);
+}
+
+int wam_plan_create_ex(wam_plan** out, int ndim, const int64_t* shape, int levels, const double* dec_lo,
+                       const double* dec_hi, const double* rec_lo, const double* rec_hi, int L, int mode,
+                       int flags) {
+  if (!out || !shape || !dec_lo || !dec_hi || !rec_lo || !rec_hi) return WAM_ERR_INVALID_ARG;
+  if (ndim < 1 || ndim > WAM_MAX_NDIM || levels < 1 || levels > WAM_MAX_LEVELS) return WAM_ERR_INVALID_ARG;
+  if (L < 2 || L > WAM_MAX_FILT || (L & 1)) return WAM_ERR_UNSUPPORTED;
+  if (mode < WAM_MODE_ZERO || mode > WAM_MODE_PERIODIC) return WAM_ERR_INVALID_ARG;
+  wam_plan* p = (wam_plan*)calloc(1, sizeof(wam_plan));
+  if (!p) return WAM_ERR_NO_MEMORY;
+  p->ndim = ndim;
+  p->levels = levels;
+  p->L = L;
+  p->mode = mode;
+  p->flags = flags;
+  p->pad = (2 * L - 3) / 2;
+  for (int a = 0; a < ndim; ++a) {
+    if (shape[a] < 1) { free(p); return WAM_ERR_SHAPE; }
+    p->shape[a] = shape[a];
+  }
+  // analysis sizes per level
+  for (int a = 0; a < ndim; ++a) {
+    int64_t n = shape[a];
+    for (int l = 0; l < levels; ++l) {
+      p->lin[l][a] = n;
+      int64_t m = (n + 2 * p->pad + (n % 2) - L) / 2 + 1;
+      if (m < 1) { free(p); return WAM_ERR_SHAPE; }
+      p->lout[l][a] = m;
+      n = m;
+    }
+  }
+  // synthesis crop flags: level l (0 finest) reconstructs 2m-2+L-2p samples; when a finer level
+  // exists its detail length decides whether one more sample is cropped at the end.
+  for (int l = levels - 1; l >= 0; --l) {
+    for (int a = 0; a < ndim; ++a) {
+      int64_t pred = 2 * p->lout[l][a] - 2 + L - 2 * p->pad;
+      int e = 0;
+      if (l > 0) {
+        int64_t next = p->lout[l - 1][a];
+        if (next == pred - 1) e = 1;
+        else if (next != pred) { free(p); return WAM_ERR_SHAPE; }
+      } else {
+        p->rec_shape[a] = pred;
+      }
+      p->extra[l][a] = e;
+    }
+  }
+  // bands
+  int per = (1 << ndim) - 1;
+  p->nbands = 1 + levels * per;
+  int64_t off = 0;
+  for (int b = 0; b < p->nbands; ++b) {
+    int lvl = (b == 0) ? levels - 1 : levels - 1 - (b - 1) / per;
+    for (int a = 0; a < ndim; ++a) p->band_dims[b][a] = p->lout[lvl][a];
+    p->band_off[b] = off;
+    off += wam_prod(p->band_dims[b], ndim);
+  }
+  p->band_off[p->nbands] = off;
+  // filters (fp32, as ptwt casts the pywt float64 tables to the data dtype)
+  for (int k = 0; k < L; ++k) {
+    p->h_filt[WAM_F_ANA_LO][k] = (float)dec_lo[L - 1 - k];
+    p->h_filt[WAM_F_ANA_HI][k] = (float)dec_hi[L - 1 - k];
+    p->h_filt[WAM_F_SYN_LO][k] = (float)rec_lo[k];
+    p->h_filt[WAM_F_SYN_HI][k] = (float)rec_hi[k];
+    p->h_filt[WAM_F_ADJ_LO][k] = (float)rec_lo[k];
+    p->h_filt[WAM_F_ADJ_HI][k] = (float)rec_hi[k];
+  }
+  hipError_t e = hipGetDevice(&p->device);
+  if (e != hipSuccess) { free(p); return WAM_ERR_HIP_BASE + (int)e; }
+  e = hipMalloc((void**)&p->d_filt, sizeof(float) * WAM_F_COUNT * L);
+  if (e != hipSuccess) { free(p); return WAM_ERR_HIP_BASE + (int)e; }
+  std::vector<float> packed(WAM_F_COUNT * L);
+  for (int f = 0; f < WAM_F_COUNT; ++f)
+    for (int k = 0; k < L; ++k) packed[f * L + k] = p->h_filt[f][k];
+  e = hipMemcpy(p->d_filt, packed.data(), sizeof(float) * packed.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { (void)hipFree(p->d_filt); free(p); return WAM_ERR_HIP_BASE + (int)e; }
+  *out = p;
+  return WAM_OK;
+}
+
+void wam_plan_destroy(wam_plan* p) {
+  if (!p) return;
+  if (p->d_filt) (void)hipFree(p->d_filt);
+  free(p);
+}
+
+int wam_plan_num_bands(const wam_plan* p) { return p ? p->nbands : -WAM_ERR_INVALID_ARG; }
+
+int wam_plan_band_shape(const wam_plan* p, int band, int64_t* dims) {
+  if (!p || !dims || band < 0 || band >= p->nbands) return WAM_ERR_INVALID_ARG;
+  for (int a = 0; a < p->ndim; ++a) dims[a] = p->band_dims[band][a];
+  return WAM_OK;
+}
+
+int64_t wam_plan_band_offset(const wam_plan* p, int band) {
+  if (!p || band < 0 || band > p->nbands) return -1;
+  return p->band_off[band];
+}
+
+int64_t wam_plan_coeff_numel(const wam_plan* p) { return p ? p->band_off[p->nbands] : -1; }
+
+int wam_plan_rec_shape(const wam_plan* p, int64_t* dims) {
+  if (!p || !dims) return WAM_ERR_INVALID_ARG;
+  for (int a = 0; a < p->ndim; ++a) dims[a] = p->rec_shape[a];
+  return WAM_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// Generic separable drivers (per-axis kernels). Axis passes go from the last axis to the first;
+// intermediate results live in the workspace.
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+// Size (elements) of the largest intermediate set of one generic analysis level.
+int64_t generic_level_tmp(const wam_plan* p, const int64_t* in_dims, const int64_t* out_dims, int64_t batch) {
+  int nd = p->ndim;
+  int64_t best = 0;
+  int64_t dims[WAM_MAX_NDIM];
+  for (int a = 0; a < nd; ++a) dims[a] = in_dims[a];
+  int parts = 1;
+  for (int ax = nd - 1; ax >= 1; --ax) {  // the last pass (ax 0) writes the final outputs
+    dims[ax] = out_dims[ax];
+    parts *= 2;
+    best += parts * batch * wam_prod(dims, nd);
+  }
+  return best;
+}
+
+int64_t generic_syn_tmp(const wam_plan* p, int64_t batch) {
+  int nd = p->ndim;
+  int64_t best = 0;
+  for (int l = p->levels - 1; l >= 0; --l) {
+    int64_t dims[WAM_MAX_NDIM];
+    for (int a = 0; a < nd; ++a) dims[a] = p->lout[l][a];
+    int parts = 1 << nd;
+    int64_t tot = 0;
+    for (int ax = nd - 1; ax >= 1; --ax) {
+      dims[ax] = 2 * p->lout[l][ax] - 2 + p->L - 2 * p->pad - p->extra[l][ax];
+      parts /= 2;
+      tot += parts * batch * wam_prod(dims, nd);
+    }
+    if (tot > best) best = tot;
+  }
+  return best;
+}
+
+int sub_of_key(int nd, int key) {
+  if (nd == 2) return key == 2 ? 0 : (key == 1 ? 1 : 2);  // (H='da', V='ad', D='dd')
+  return key - 1;
+}
+
+}  // namespace
+
+extern "C" int64_t wam_plan_workspace_bytes(const wam_plan* p, int64_t batch) {
+  if (!p || batch < 0) return -1;
+  int nd = p->ndim;
+  // LL ping-pong for analysis / adjoint (level 0 output) and A ping-pong for synthesis
+  int64_t ll = batch * wam_prod(p->lout[0], nd);
+  int64_t rec_ll = 0;
+  for (int l = p->levels - 1; l >= 1; --l) {
+    int64_t d[WAM_MAX_NDIM];
+    for (int a = 0; a < nd; ++a) d[a] = p->lout[l - 1][a];
+    int64_t v = batch * wam_prod(d, nd);
+    if (v > rec_ll) rec_ll = v;
+  }
+  int64_t tmp_a = 0;
+  int64_t rec0[WAM_MAX_NDIM];
+  for (int a = 0; a < nd; ++a) rec0[a] = p->rec_shape[a];
+  for (int l = 0; l < p->levels; ++l) {
+    int64_t v = generic_level_tmp(p, l == 0 ? rec0 : p->lin[l], p->lout[l], batch);
+    int64_t v2 = generic_level_tmp(p, p->lin[l], p->lout[l], batch);
+    if (v > tmp_a) tmp_a = v;
+    if (v2 > tmp_a) tmp_a = v2;
+  }
+  int64_t tmp_s = generic_syn_tmp(p, batch);
+  int64_t a_side = 2 * ll + tmp_a;
+  int64_t s_side = 2 * rec_ll + tmp_s;
+  int64_t elems = a_side > s_side ? a_side : s_side;
+  return (elems + 64) * (int64_t)sizeof(float);
+}
+
+namespace {
+
+// One analysis level over arbitrary ndim via per-axis passes. `in` has dims in_dims; outputs:
+// approx -> out_a, details -> bands (pointers per sub index).
+int generic_analysis_level(const wam_plan* p, int64_t batch, const float* in, const int64_t* in_dims,
+                           const int64_t* out_dims, int mode, int fset, float* out_a, float* const* out_sub,
+                           float* tmp, hipStream_t st) {
+  int nd = p->ndim;
+  const float* flo = p->d_filt + (fset + 0) * p->L;
+  const float* fhi = p->d_filt + (fset + 1) * p->L;
+  // parts: (key, pointer, dims)
+  struct Part { int key; const float* ptr; };
+  Part cur[8], nxt[8];
+  int ncur = 1;
+  cur[0] = {0, in};
+  int64_t dims[WAM_MAX_NDIM];
+  for (int a = 0; a < nd; ++a) dims[a] = in_dims[a];
+  float* tcur = tmp;
+  for (int ax = nd - 1; ax >= 0; --ax) {
+    int64_t outer = batch;
+    for (int a = 0; a < ax; ++a) outer *= dims[a];
+    int64_t inner = 1;
+    for (int a = ax + 1; a < nd; ++a) inner *= dims[a];
+    int n = (int)dims[ax];
+    int m = (int)out_dims[ax];
+    int64_t odims[WAM_MAX_NDIM];
+    for (int a = 0; a < nd; ++a) odims[a] = dims[a];
+    odims[ax] = m;
+    int64_t part_elems = batch * wam_prod(odims, nd);
+    int bit = 1 << (nd - 1 - ax);
+    for (int i = 0; i < ncur; ++i) {
+      float* lo;
+      float* hi;
+      int klo = cur[i].key, khi = cur[i].key | bit;
+      if (ax == 0) {
+        lo = (klo == 0) ? out_a : out_sub[sub_of_key(nd, klo)];
+        hi = out_sub[sub_of_key(nd, khi)];
+      } else {
+        lo = tcur;
+        hi = tcur + part_elems;
+        tcur += 2 * part_elems;
+      }
+      int rc = launch_analysis_axis(cur[i].ptr, lo, hi, outer, n, m, inner, p->pad, mode, flo, fhi, p->L, st);
+      if (rc) return rc;
+      nxt[2 * i] = {klo, lo};
+      nxt[2 * i + 1] = {khi, hi};
+    }
+    ncur *= 2;
+    for (int i = 0; i < ncur; ++i) cur[i] = nxt[i];
+    for (int a = 0; a < nd; ++a) dims[a] = odims[a];
+  }
+  return WAM_OK;
+}
+
+// One synthesis level (c_pos order handled by the caller). a_in: approximation (band or previous
+// output), sub[k]: detail bands; out: cropped result.
+int generic_synthesis_level(const wam_plan* p, int64_t batch, int level, const float* a_in, float a_scale,
+                            const float* const* sub, float d_scale, float* out, float* tmp, hipStream_t st) {
+  int nd = p->ndim;
+  const float* rlo = p->d_filt + WAM_F_SYN_LO * p->L;
+  const float* rhi = p->d_filt + WAM_F_SYN_HI * p->L;
+  struct Part { int key; const float* ptr; float scale; };
+  Part cur[8];
+  int ncur = 1 << nd;
+  for (int key = 0; key < ncur; ++key) {
+    if (key == 0) cur[key] = {0, a_in, a_scale};
+    else cur[key] = {key, sub[sub_of_key(nd, key)], d_scale};
+  }
+  int64_t dims[WAM_MAX_NDIM];
+  for (int a = 0; a < nd; ++a) dims[a] = p->lout[level][a];
+  float* tcur = tmp;
+  for (int ax = nd - 1; ax >= 0; --ax) {
+    int64_t outer = batch;
+    for (int a = 0; a < ax; ++a) outer *= dims[a];
+    int64_t inner = 1;
+    for (int a = ax + 1; a < nd; ++a) inner *= dims[a];
+    int m = (int)dims[ax];
+    int nout = (int)(2 * dims[ax] - 2 + p->L - 2 * p->pad - p->extra[level][ax]);
+    int64_t odims[WAM_MAX_NDIM];
+    for (int a = 0; a < nd; ++a) odims[a] = dims[a];
+    odims[ax] = nout;
+    int64_t part_elems = batch * wam_prod(odims, nd);
+    int bit = 1 << (nd - 1 - ax);
+    Part nxt[8];
+    int nn = 0;
+    for (int i = 0; i < ncur; ++i) {
+      if (cur[i].key & bit) continue;
+      const Part* pa = &cur[i];
+      const Part* pd = nullptr;
+      for (int j = 0; j < ncur; ++j)
+        if (cur[j].key == (cur[i].key | bit)) pd = &cur[j];
+      float* dst = (ax == 0) ? out : tcur;
+      if (ax != 0) tcur += part_elems;
+      int rc = launch_synthesis_axis(pa->ptr, pd->ptr, dst, outer, m, nout, inner, p->pad, rlo, rhi, p->L,
+                                     pa->scale, pd->scale, st);
+      if (rc) return rc;
+      nxt[nn++] = {cur[i].key, dst, 1.0f};
+    }
+    ncur = nn;
+    for (int i = 0; i < ncur; ++i) cur[i] = nxt[i];
+    for (int a = 0; a < nd; ++a) dims[a] = odims[a];
+  }
+  return WAM_OK;
+}
+
+void band_ptrs(const wam_plan* p, int64_t batch, float* coeffs, int level, float** sub) {
+  int per = (1 << p->ndim) - 1;
+  for (int k = 0; k < per; ++k) sub[k] = coeffs + batch * p->band_off[wam_band_of(p, level, k)];
+}
+
+int analysis_driver(const wam_plan* p, int64_t batch, const float* x, float* coeffs, void* ws, hipStream_t st,
+                    bool adjoint) {
+  int nd = p->ndim;
+  float* w = (float*)ws;
+  int64_t ll = batch * wam_prod(p->lout[0], nd);
+  float* llbuf[2] = {w, w + ll};
+  float* tmp = w + 2 * ll;
+  const float* cur = x;
+  int mode = adjoint ? WAM_MODE_ZERO : p->mode;
+  int fset = adjoint ? WAM_F_ADJ_LO : WAM_F_ANA_LO;
+  for (int l = 0; l < p->levels; ++l) {
+    int64_t in_dims[WAM_MAX_NDIM];
+    for (int a = 0; a < nd; ++a) in_dims[a] = (adjoint && l == 0) ? p->rec_shape[a] : p->lin[l][a];
+    float* sub[7];
+    band_ptrs(p, batch, coeffs, l, sub);
+    float* out_a = (l == p->levels - 1) ? coeffs : llbuf[l & 1];
+    int rc;
+    if (nd == 2 && !(p->flags & WAM_PLAN_GENERIC) && dwt2_fused_supported(p)) {
+      rc = launch_dwt2_analysis_fused(p, batch, cur, in_dims, p->lout[l], mode, fset, out_a, sub, st);
+    } else {
+      rc = generic_analysis_level(p, batch, cur, in_dims, p->lout[l], mode, fset, out_a, sub, tmp, st);
+    }
+    if (rc) return rc;
+    cur = out_a;
+  }
+  return WAM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wam_wavedec(const wam_plan* p, int64_t batch, const float* x, float* coeffs, void* ws, void* stream) {
+  if (!p || !x || !coeffs || !ws || batch < 0) return WAM_ERR_INVALID_ARG;
+  if (batch == 0) return WAM_OK;
+  return analysis_driver(p, batch, x, coeffs, ws, (hipStream_t)stream, false);
+}
+
+int wam_waverec_adjoint(const wam_plan* p, int64_t batch, const float* grad, float* coeff_grads, void* ws,
+                        void* stream) {
+  if (!p || !grad || !coeff_grads || !ws || batch < 0) return WAM_ERR_INVALID_ARG;
+  if (batch == 0) return WAM_OK;
+  return analysis_driver(p, batch, grad, coeff_grads, ws, (hipStream_t)stream, true);
+}
+
+int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha, int n_alpha, float* out,
+                void* ws, void* stream) {
+  if (!p || !coeffs || !out || !ws || batch < 0 || n_alpha < 1) return WAM_ERR_INVALID_ARG;
+  if (!alpha && n_alpha != 1) return WAM_ERR_INVALID_ARG;
+  if (batch == 0) return WAM_OK;
+  hipStream_t st = (hipStream_t)stream;
+  int nd = p->ndim;
+  int64_t out_item = wam_prod(p->rec_shape, nd);
+  int64_t rec_ll = 0;
+  for (int l = p->levels - 1; l >= 1; --l) {
+    int64_t v = batch * wam_prod(p->lout[l - 1], nd);
+    if (v > rec_ll) rec_ll = v;
+  }
+  float* w = (float*)ws;
+  float* abuf[2] = {w, w + rec_ll};
+  float* tmp = w + 2 * rec_ll;
+  for (int ai = 0; ai < n_alpha; ++ai) {
+    float s = alpha ? alpha[ai] : 1.0f;
+    const float* a_cur = coeffs;  // band 0 = A_J
+    float a_scale = s;
+    for (int c = 0; c < p->levels; ++c) {
+      int l = p->levels - 1 - c;
+      float* sub[7];
+      band_ptrs(p, batch, (float*)coeffs, l, sub);
+      float* dst = (l == 0) ? out + (int64_t)ai * batch * out_item : abuf[c & 1];
+      int rc;
+      if (nd == 2 && !(p->flags & WAM_PLAN_GENERIC) && dwt2_fused_supported(p)) {
+        rc = launch_dwt2_synthesis_fused(p, batch, l, a_cur, a_scale, sub, s, dst, st);
+      } else {
+        rc = generic_synthesis_level(p, batch, l, a_cur, a_scale, sub, s, dst, tmp, st);
+      }
+      if (rc) return rc;
+      a_cur = dst;
+      a_scale = 1.0f;
+    }
+  }
+  return WAM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,141 @@
+"""Shared host logic of the WAM classes: device placement, the model's input gradient with the
+reference's loss semantics, SmoothGrad noise streams, sample / step sharding across ranks.
+
+Loss (lib/wam_2D.py:115, lib/wam_1D.py:125, lib/wam_3D.py:237): ``torch.diag(output[:, y]).mean()``.
+For an int y its gradient is 1/N^2 on out[i, y]; for a sequence it is 1/N on out[i, y_i]. Several
+noise samples (or IG steps) are stacked into ONE model batch of groups x N images; the loss is the
+sum of the per-group losses, so each group gets exactly the gradient of its own reference call
+(models must not couple batch items -- eval-mode BatchNorm is fine; training-mode models are run
+one group per call).
+Only the input gradient is computed (torch.autograd.grad): the reference's parameter-.grad
+accumulation side effect is not reproduced.
+"""
+import contextlib
+
+import numpy as np
+import torch
+import torch.distributed as tdist
+
+
+def model_device(model, device=None):
+    if device is not None:
+        return torch.device(device)
+    return next(model.parameters()).device
+
+
+def require_gpu_device(device):
+    device = torch.device(device)
+    if device.type != "cuda":
+        raise RuntimeError("wam_amd runs the WAM path on the GPU only; the explained model lives on %s. "
+                           "Pass device='cuda' or move the model to a HIP device." % device)
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    return device
+
+
+def _is_int_label(y):
+    return isinstance(y, (int, np.integer)) or (isinstance(y, torch.Tensor) and y.dim() == 0)
+
+
+def seed_gradient(out, y, groups, n):
+    """d loss / d out for `groups` stacked reference calls of n items each."""
+    go = torch.zeros_like(out, dtype=torch.float32)
+    rows = torch.arange(groups * n, device=out.device)
+    if _is_int_label(y):
+        val = torch.tensor(1.0, dtype=torch.float32) / (n * n)
+        go[rows, int(y)] = val.to(out.device)
+    else:
+        yy = torch.as_tensor(np.asarray([int(v) for v in (y.tolist() if isinstance(y, torch.Tensor) else y)]),
+                             dtype=torch.long)
+        if yy.numel() != n:
+            # the reference's diag(output[:, y]) with len(y) != N takes min(N, len(y)) entries
+            k = min(n, yy.numel())
+            val = torch.tensor(1.0, dtype=torch.float32) / k
+            sel = torch.arange(k)
+            rr = (torch.arange(groups)[:, None] * n + sel[None, :]).reshape(-1)
+            cc = yy[:k].repeat(groups)
+            go[rr.to(out.device), cc.to(out.device)] = val.to(out.device)
+            return go.to(out.dtype)
+        val = torch.tensor(1.0, dtype=torch.float32) / n
+        go[rows, yy.repeat(groups).to(out.device)] = val.to(out.device)
+    return go.to(out.dtype)
+
+
+def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=False, y_none_mean=False):
+    """Gradient of the summed per-group reference losses w.r.t. img (fp32)."""
+    img = img.detach().requires_grad_(True)
+    inp = img.contiguous(memory_format=torch.channels_last) if channels_last and img.dim() == 4 else img
+    ctx = torch.autocast("cuda", dtype=autocast_dtype) if autocast_dtype is not None else contextlib.nullcontext()
+    with ctx:
+        out = model(inp)
+    if y_none_mean:
+        loss = out.float().mean()
+        (g,) = torch.autograd.grad(loss, img)
+    else:
+        (g,) = torch.autograd.grad(out, img, grad_outputs=seed_gradient(out, y, groups, n))
+    return g.contiguous()
+
+
+def legacy_noise(sigmas, item_shape, seed, samples, n_total=None):
+    """The reference's stream (lib/wam_2D.py:385-403): np.random.seed(seed) then, for every sample
+    and item in order, np.random.normal(0, sigma_i, item_shape) in float64 cast to float32.
+    Yields (s, float32 array [items, *item_shape]) for s in `samples` (a sorted list); earlier
+    samples are generated and discarded so the stream position is identical on every rank.
+    Uses (and leaves advanced) the global numpy RNG, exactly like the reference."""
+    np.random.seed(seed)
+    want = set(samples)
+    last = max(samples) if samples else -1
+    for s in range(last + 1):
+        arr = np.empty((len(sigmas),) + tuple(item_shape), dtype=np.float32)
+        for i, sg in enumerate(sigmas):
+            arr[i] = np.random.normal(0, sg, tuple(item_shape)).astype(np.float32)
+        if s in want:
+            yield s, arr
+
+
+# ------------------------------------------------------------------------------ distribution
+class Shard:
+    """Which noise samples / IG steps this process evaluates, and how partial results combine.
+    dist=None/False: everything local. dist=True: the default torch.distributed group (RCCL on
+    ROCm for cuda tensors); or pass a ProcessGroup."""
+
+    def __init__(self, dist=None):
+        if dist is None or dist is False or not (tdist.is_available() and tdist.is_initialized()):
+            self.group, self.rank, self.world = None, 0, 1
+        else:
+            self.group = None if dist is True else dist
+            self.rank = tdist.get_rank(self.group)
+            self.world = tdist.get_world_size(self.group)
+
+    def range(self, n):
+        """Contiguous block of [0, n) for this rank (ragged: the first n % world ranks get one more)."""
+        q, r = divmod(n, self.world)
+        start = self.rank * q + min(self.rank, r)
+        return start, start + q + (1 if self.rank < r else 0)
+
+    def all_reduce_sum(self, t):
+        if self.world > 1:
+            tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def all_reduce_max(self, t):
+        if self.world > 1:
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX, group=self.group)
+        return t
+
+
+def chunks(start, stop, size):
+    out = []
+    s = start
+    while s < stop:
+        out.append((s, min(size, stop - s)))
+        s += size
+    return out
+
+
+def auto_group(model, n_items, requested, cap_items=256):
+    if requested is not None:
+        return max(1, int(requested))
+    if getattr(model, "training", False):
+        return 1
+    return max(1, cap_items // max(1, n_items))

@@ -1,0 +1,208 @@
+"""Python side of the C-ABI: plans (cached per device) and thin typed wrappers of every entry
+point of include/wam_hip.h. torch allocates every device buffer; every call is asynchronous on
+torch's current stream of the tensor's device."""
+import ctypes
+import threading
+
+import numpy as np
+import torch
+
+from . import filters
+from ._lib import c_f32, c_i64, c_vp, check, lib, ptr, require_cuda, stream_of
+
+_CACHE = {}
+_LOCK = threading.Lock()
+PLAN_GENERIC = 1
+
+
+class Plan:
+    """Immutable transform plan (ndim, spatial shape, levels, wavelet, mode) on one device."""
+
+    def __init__(self, ndim, shape, levels, wavelet, mode, device, flags=0):
+        self.ndim = int(ndim)
+        self.shape = tuple(int(s) for s in shape)
+        self.levels = int(levels)
+        self.wavelet = filters.get_wavelet(wavelet)
+        self.mode = mode
+        self.device = torch.device(device)
+        self.flags = flags
+        L = len(self.wavelet.dec_lo)
+        arr = lambda v: (ctypes.c_double * L)(*v)
+        shp = (ctypes.c_int64 * self.ndim)(*self.shape)
+        handle = c_vp()
+        with torch.cuda.device(self.device):
+            check(lib.wam_plan_create_ex(ctypes.byref(handle), self.ndim, shp, self.levels, arr(self.wavelet.dec_lo),
+                                         arr(self.wavelet.dec_hi), arr(self.wavelet.rec_lo),
+                                         arr(self.wavelet.rec_hi), L, filters.mode_id(mode), flags))
+        self._h = handle
+        self.L = L
+        self.nbands = lib.wam_plan_num_bands(handle)
+        dims = (ctypes.c_int64 * self.ndim)()
+        self.band_shapes = []
+        for b in range(self.nbands):
+            check(lib.wam_plan_band_shape(handle, b, dims))
+            self.band_shapes.append(tuple(dims[:]))
+        self.band_offsets = [lib.wam_plan_band_offset(handle, b) for b in range(self.nbands + 1)]
+        self.coeff_numel = lib.wam_plan_coeff_numel(handle)
+        check(lib.wam_plan_rec_shape(handle, dims))
+        self.rec_shape = tuple(dims[:])
+        self._ws = {}
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and lib is not None:
+            lib.wam_plan_destroy(h)
+            self._h = None
+
+    # ---------------------------------------------------------------- layout helpers
+    @property
+    def handle(self):
+        return self._h
+
+    def workspace(self, batch):
+        n = int(lib.wam_plan_workspace_bytes(self._h, batch))
+        ws = self._ws.get("buf")
+        if ws is None or ws.numel() < n:
+            ws = torch.empty(n, dtype=torch.uint8, device=self.device)
+            self._ws["buf"] = ws
+        return ws
+
+    def split(self, flat, batch, lead=None):
+        """Band views of a band-major coefficient buffer; each band reshaped to lead + band dims."""
+        lead = (batch,) if lead is None else tuple(lead)
+        out = []
+        for b in range(self.nbands):
+            n = int(np.prod(self.band_shapes[b]))
+            o = batch * self.band_offsets[b]
+            out.append(flat[o:o + batch * n].view(lead + self.band_shapes[b]))
+        return out
+
+    def band_level(self, b):
+        """(level index 0 = finest, sub index) of band b; approximation -> (levels-1, -1)."""
+        if b == 0:
+            return self.levels - 1, -1
+        per = (1 << self.ndim) - 1
+        return self.levels - 1 - (b - 1) // per, (b - 1) % per
+
+    # ---------------------------------------------------------------- transforms
+    def wavedec(self, x, out=None):
+        """x: [batch, *shape] fp32 cuda -> band-major flat coefficients [batch * coeff_numel]."""
+        require_cuda(x, "x")
+        x = x.contiguous()
+        batch = x.numel() // int(np.prod(self.shape))
+        if tuple(x.shape[-self.ndim:]) != self.shape:
+            raise ValueError("input spatial shape %s does not match the plan %s" % (tuple(x.shape), self.shape))
+        if out is None:
+            out = torch.empty(batch * self.coeff_numel, dtype=torch.float32, device=x.device)
+        ws = self.workspace(batch)
+        check(lib.wam_wavedec(self._h, batch, ptr(x), ptr(out), ptr(ws), stream_of(x.device)))
+        return out
+
+    def waverec(self, flat, batch, alphas=None, out=None):
+        """flat band-major coefficients -> [n_alpha, batch, *rec_shape] (n_alpha = 1 without alphas)."""
+        require_cuda(flat, "coefficients")
+        n_alpha = 1 if alphas is None else len(alphas)
+        a = None if alphas is None else (c_f32 * n_alpha)(*[float(np.float32(v)) for v in alphas])
+        if out is None:
+            out = torch.empty((n_alpha, batch) + self.rec_shape, dtype=torch.float32, device=flat.device)
+        ws = self.workspace(batch)
+        check(lib.wam_waverec(self._h, batch, ptr(flat.contiguous()), a, n_alpha, ptr(out), ptr(ws),
+                              stream_of(flat.device)))
+        return out
+
+    def adjoint(self, grad, out=None):
+        """grad [batch, *rec_shape] -> band-major coefficient gradients (waverec's VJP)."""
+        require_cuda(grad, "grad")
+        grad = grad.contiguous()
+        batch = grad.numel() // int(np.prod(self.rec_shape))
+        if out is None:
+            out = torch.empty(batch * self.coeff_numel, dtype=torch.float32, device=grad.device)
+        ws = self.workspace(batch)
+        check(lib.wam_waverec_adjoint(self._h, batch, ptr(grad), ptr(out), ptr(ws), stream_of(grad.device)))
+        return out
+
+
+def get_plan(ndim, shape, levels, wavelet, mode, device, generic=False):
+    w = filters.get_wavelet(wavelet)
+    device = torch.device(device)
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    key = (ndim, tuple(int(s) for s in shape), int(levels), w, mode, device, bool(generic))
+    with _LOCK:
+        p = _CACHE.get(key)
+        if p is None:
+            p = Plan(ndim, shape, levels, w, mode, device, PLAN_GENERIC if generic else 0)
+            _CACHE[key] = p
+    return p
+
+
+# -------------------------------------------------------------------- WAM epilogue wrappers
+def item_sigma(x, item_stride, length, spread):
+    items = x.numel() // item_stride
+    sigma = torch.empty(items, dtype=torch.float32, device=x.device)
+    check(lib.wam_item_sigma(items, item_stride, length, ptr(x), float(np.float32(spread)), ptr(sigma),
+                             stream_of(x.device)))
+    return sigma
+
+
+def noise_add(x, sigma, n_samples, items, item_stride, noised_len, seed=0, sample_base=0, host_noise=None, out=None):
+    if out is None:
+        out = torch.empty((n_samples * items * item_stride,), dtype=torch.float32, device=x.device)
+    check(lib.wam_noise_add(n_samples, items, item_stride, noised_len, ptr(x), ptr(sigma), ptr(host_noise),
+                            ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), sample_base, ptr(out), stream_of(x.device)))
+    return out
+
+
+def subband_maps(plan, coeff_grads, groups, group_items, channels, maps=None, band_max=None):
+    items = groups * group_items
+    dev = coeff_grads.device
+    if maps is None:
+        maps = torch.empty(items * plan.coeff_numel, dtype=torch.float32, device=dev)
+    if band_max is None:
+        band_max = torch.zeros((groups, plan.nbands), dtype=torch.float32, device=dev)
+    else:
+        band_max.zero_()
+    check(lib.wam_subband_maps(plan.handle, groups, group_items, channels, ptr(coeff_grads), ptr(maps), ptr(band_max),
+                               stream_of(dev)))
+    return maps, band_max
+
+
+def frame_accumulate(groups, group_items, gmap, maps, maps_item_len, band_max, n_bands, normalize, frame):
+    src, band = gmap
+    check(lib.wam_frame_accumulate(groups, group_items, src.numel(), ptr(src), ptr(band), ptr(maps), maps_item_len,
+                                   ptr(band_max), n_bands, int(bool(normalize)), ptr(frame), stream_of(frame.device)))
+
+
+def frame_trapz(groups, k0, group_items, gmap, maps, maps_item_len, band_max, n_bands, normalize, prev, acc,
+                weights=None):
+    src, band = gmap
+    check(lib.wam_frame_trapz(groups, k0, group_items, src.numel(), ptr(src), ptr(band), ptr(maps), maps_item_len,
+                              ptr(band_max), n_bands, int(bool(normalize)), ptr(weights), ptr(prev), ptr(acc),
+                              stream_of(acc.device)))
+
+
+def cube_accumulate(groups, k0, group_items, src, maps, maps_item_len, mode, n_total, acc, prev=None, weights=None):
+    check(lib.wam_cube_accumulate(groups, k0, group_items, src.numel(), ptr(src), ptr(maps), maps_item_len, mode,
+                                  float(n_total), ptr(weights), ptr(prev), ptr(acc), stream_of(acc.device)))
+
+
+def accumulate_f32(src, groups, acc, scale=0.0):
+    check(lib.wam_accumulate_f32(groups, acc.numel(), ptr(src), float(scale), ptr(acc), stream_of(acc.device)))
+
+
+def trapz_stream(src, groups, k0, prev, acc, weights=None):
+    if acc.dtype == torch.float64:
+        check(lib.wam_trapz_f32(groups, k0, acc.numel(), ptr(src), ptr(weights), None, None, ptr(prev), ptr(acc),
+                                stream_of(acc.device)))
+    else:
+        check(lib.wam_trapz_f32(groups, k0, acc.numel(), ptr(src), ptr(weights), ptr(prev), ptr(acc), None, None,
+                                stream_of(acc.device)))
+
+
+def reproject_scales(avg, levels, approx):
+    """avg: [items, size, size] float64 cuda -> [items, levels(+1), size, size] float64."""
+    items, size = avg.shape[0], avg.shape[1]
+    out = torch.empty((items, levels + (1 if approx else 0), size, size), dtype=torch.float64, device=avg.device)
+    check(lib.wam_reproject_scales(items, size, levels, int(bool(approx)), ptr(avg.contiguous()), ptr(out),
+                                   stream_of(avg.device)))
+    return out

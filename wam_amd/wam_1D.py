@@ -1,0 +1,256 @@
+"""WAM for audio on MI355X: drop-in for the reference's ``lib/wam_1D.py`` attribution classes.
+
+``BaseWAM1D`` (lib/wam_1D.py:54-246) and ``WaveletAttribution1D`` (:249-435) with the same
+constructor arguments, ``__call__`` signatures, returns ``(melspec gradients, [coefficient
+gradients per level])`` and side attributes (``wavelet_coeffs``, ``gradient_coeffs``,
+``melspecs``, ``grad_coeffs``, ``rates``). wavedec / waverec / the adjoint, the SmoothGrad noise,
+the IG path scaling and the sample accumulators are HIP kernels; the mel front-end is a batched
+torch.stft on the GPU (wam_amd/melspec.py). Build-only kwargs as in wam_amd.wam_2D (noise,
+sample_batch, autocast_dtype, dist).
+"""
+import numpy as np
+import torch
+
+from .engine import Shard, auto_group, chunks, input_gradient, legacy_noise, model_device, require_gpu_device
+from .melspec import melspec_db
+from .plan import accumulate_f32, get_plan, item_sigma, noise_add, trapz_stream
+
+
+def _peak_normalise(x):
+    return torch.tensor(np.array([wf / wf.max() for wf in x]).astype(np.float32))
+
+
+class BaseWAM1D:
+    def __init__(self, model, wavelet="haar", J=2, mode="symmetric", device=None, approx_coeffs=False, n_mels=128,
+                 n_fft=1024, sample_rate=44100, *, autocast_dtype=None):
+        self.wavelet = wavelet
+        self.J = J
+        self.mode = mode
+        self.approx_coeffs = approx_coeffs
+        self.n_mels = n_mels
+        self.n_fft = n_fft
+        self.sample_rate = sample_rate
+        if device is not None:
+            model = model.to(device)
+            self.model = model
+            self.device = device
+        else:
+            self.model = model
+            self.device = next(model.parameters()).device
+        self.autocast_dtype = autocast_dtype
+        self._pass = None
+        self._wc = None
+        self._gc = None
+
+    @property
+    def _dev(self):
+        return require_gpu_device(model_device(self.model, self.device))
+
+    # ------------------------------------------------------------------ lazy side attributes
+    def _split_np(self, plan, flat, items, first, n):
+        return [v[first:first + n].detach().cpu().numpy() for v in plan.split(flat, items)]
+
+    @property
+    def wavelet_coeffs(self):
+        if self._wc is None and self._pass is not None:
+            plan, (cf, ci, c0), _, n = self._pass
+            self._wc = self._split_np(plan, cf, ci, c0, n)
+        return self._wc
+
+    @wavelet_coeffs.setter
+    def wavelet_coeffs(self, v):
+        self._wc = v
+
+    @property
+    def gradient_coeffs(self):
+        if self._gc is None and self._pass is not None:
+            plan, _, (gf, gi, g0), n = self._pass
+            self._gc = self._split_np(plan, gf, gi, g0, n)
+        return self._gc
+
+    @gradient_coeffs.setter
+    def gradient_coeffs(self, v):
+        self._gc = v
+
+    def _record(self, plan, cf, ci, c0, gf, gi, g0, n):
+        self._pass = (plan, (cf, ci, c0), (gf, gi, g0), n)
+        self._wc = self._gc = None
+
+    # ------------------------------------------------------------------ core pass (batched groups)
+    def _grads(self, plan, flat, items, y, groups, n):
+        """waverec -> melspec -> model -> (melspec grad [items,1,T,M], coefficient grads flat)."""
+        rec = plan.waverec(flat, items)[0]
+        rec_leaf = rec.detach().requires_grad_(True)
+        with torch.enable_grad():
+            mel = melspec_db(rec_leaf, self.n_fft, self.sample_rate, self.n_mels)
+        g_mel = input_gradient(self.model, mel.detach(), y, groups, n, self.autocast_dtype)
+        (g_rec,) = torch.autograd.grad(mel, rec_leaf, grad_outputs=g_mel)
+        cg = plan.adjoint(g_rec.contiguous())
+        return g_mel, cg
+
+    def compute_melspec(self, reconstruction, n_fft=1024, sample_rate=44100, n_mels=128):
+        """lib/wam_1D.py:194-219: [N, W] -> [N, 1, T, n_mels] (on the GPU)."""
+        rec = torch.as_tensor(reconstruction)
+        rec = rec.to(self._dev, torch.float32) if rec.device.type != "cuda" else rec
+        return melspec_db(rec, n_fft, sample_rate, n_mels)
+
+    def __call__(self, x, y, rates=None, waveform=True):
+        self.rates = rates
+        dev = self._dev
+        if waveform:
+            if isinstance(x, list):
+                x = _peak_normalise(x)
+            x = x.detach().to(dev, torch.float32).contiguous()
+            n, w = x.shape
+            plan = get_plan(1, (w,), self.J, self.wavelet, self.mode, dev)
+            flat = plan.wavedec(x)
+        else:
+            coeffs = list(x)
+            n = coeffs[0].shape[0]
+            from .filters import get_wavelet
+            L = len(get_wavelet(self.wavelet).dec_lo)
+            plan = get_plan(1, (2 * coeffs[-1].shape[-1] + 2 - L,), len(coeffs) - 1, self.wavelet, self.mode, dev)
+            flat = torch.cat([c.detach().to(dev, torch.float32).reshape(-1) for c in coeffs])
+        g_mel, cg = self._grads(plan, flat, n, y, 1, n)
+        self._record(plan, flat, n, 0, cg, n, 0, n)
+        grads = [v.detach().cpu().numpy() for v in plan.split(cg, n)]
+        return g_mel.detach().cpu().numpy().squeeze(), grads
+
+    def visualize_grad_wam(self, coeffs):
+        """lib/wam_1D.py:152-192 (host numpy pseudo-scaleogram)."""
+        batch = coeffs[0].shape[0]
+        max_length = coeffs[-1].shape[1]
+        sc = np.ones((batch, self.J + 1, max_length)) * np.nan
+        for i in range(batch):
+            samples = [c[i] for c in coeffs]
+            ap = np.abs(samples[0])
+            ap /= ap.max()
+            sc[i, 0, :ap.shape[0]] = ap
+            for j, d in enumerate(samples[1:]):
+                d = np.abs(d)
+                d /= d.max()
+                sc[i, j + 1, :d.shape[0]] = d
+        return sc
+
+
+class WaveletAttribution1D(BaseWAM1D):
+    def __init__(self, model, wavelet="haar", J=3, method="smooth", mode="reflect", device=None, approx_coeffs=False,
+                 n_mels=128, n_fft=1024, sample_rate=44100, n_samples=25, stdev_spread=0.001, random_seed=42, *,
+                 noise="numpy", sample_batch=None, autocast_dtype=None, dist=None):
+        super().__init__(model, wavelet=wavelet, J=J, device=device, mode=mode, approx_coeffs=approx_coeffs,
+                         n_mels=n_mels, n_fft=n_fft, sample_rate=sample_rate, autocast_dtype=autocast_dtype)
+        self.n_samples = n_samples
+        self.stdev_spread = stdev_spread
+        self.random_seed = random_seed
+        self.method = method
+        if noise not in ("numpy", "philox"):
+            raise ValueError("noise must be 'numpy' or 'philox'")
+        self.noise = noise
+        self.sample_batch = sample_batch
+        self.dist = dist
+        self.wam = BaseWAM1D(model, wavelet=wavelet, J=J, mode=mode, device=device, approx_coeffs=approx_coeffs,
+                             n_mels=n_mels, n_fft=n_fft, sample_rate=sample_rate, autocast_dtype=autocast_dtype)
+
+    def smooth_wam(self, x, y):
+        """lib/wam_1D.py:294-343: mean over noisy samples of the raw gradients."""
+        dev = self._dev
+        if isinstance(x, list):
+            x = _peak_normalise(x)
+        x = x.detach().to(dev, torch.float32).contiguous()
+        n, w = x.shape
+        plan = get_plan(1, (w,), self.J, self.wavelet, self.mode, dev)
+        sigma = item_sigma(x, w, w, self.stdev_spread)
+        shard = Shard(self.dist)
+        s_lo, s_hi = shard.range(self.n_samples)
+        group = auto_group(self.model, n, self.sample_batch)
+        noise_it = None
+        if self.noise == "numpy":
+            noise_it = legacy_noise([float(v) for v in sigma.cpu().numpy()], (w,), self.random_seed,
+                                    list(range(s_lo, s_hi)))
+        mel_acc = None
+        c_acc = torch.zeros(n * plan.coeff_numel, dtype=torch.float32, device=dev)
+        for s0, cnt in chunks(s_lo, s_hi, group):
+            host = None
+            if noise_it is not None:
+                host = torch.from_numpy(np.stack([next(noise_it)[1] for _ in range(cnt)])).to(dev)
+            noisy = noise_add(x, sigma, cnt, n, w, w, seed=self.random_seed, sample_base=s0, host_noise=host)
+            flat = plan.wavedec(noisy.view(cnt * n, w))
+            g_mel, cg = self._grads(plan, flat, cnt * n, y, cnt, n)
+            if mel_acc is None:
+                mel_acc = torch.zeros(g_mel.numel() // cnt, dtype=torch.float32, device=dev)
+                self._mel_shape = (n,) + tuple(g_mel.shape[1:])
+            accumulate_f32(g_mel, cnt, mel_acc)
+            for b in range(plan.nbands):
+                nb = int(np.prod(plan.band_shapes[b]))
+                src = cg[cnt * n * plan.band_offsets[b]:cnt * n * (plan.band_offsets[b] + nb)]
+                accumulate_f32(src, cnt, c_acc[n * plan.band_offsets[b]:n * (plan.band_offsets[b] + nb)])
+            self.wam._record(plan, flat, cnt * n, (cnt - 1) * n, cg, cnt * n, (cnt - 1) * n, n)
+        shard.all_reduce_sum(mel_acc)
+        shard.all_reduce_sum(c_acc)
+        accumulate_f32(mel_acc, 0, mel_acc, scale=float(self.n_samples))
+        accumulate_f32(c_acc, 0, c_acc, scale=float(self.n_samples))
+        mel = mel_acc.view(self._mel_shape).cpu().numpy().squeeze()
+        avg = [v.cpu().numpy() for v in plan.split(c_acc, n)]
+        self.melspecs = mel
+        self.grad_coeffs = avg
+        return mel, avg
+
+    def alter(self, alpha, coeffs):
+        return [alpha * c for c in coeffs]
+
+    def integrated_wam(self, x, y):
+        """lib/wam_1D.py:353-421."""
+        dev = self._dev
+        if isinstance(x, list):
+            x = _peak_normalise(x)
+        x = x.detach().to(dev, torch.float32).contiguous()
+        n, w = x.shape
+        plan = get_plan(1, (w,), self.J, self.wavelet, self.mode, dev)
+        alphas = np.linspace(0, 1, self.n_samples)
+        z = plan.wavedec(x)
+        base_z = [v.cpu().numpy() for v in plan.split(z, n)]
+        base_mel = melspec_db(x, self.n_fft, self.sample_rate, self.n_mels).squeeze(1).detach()
+        shard = Shard(self.dist)
+        k_lo, k_hi = shard.range(self.n_samples)
+        group = auto_group(self.model, n, self.sample_batch)
+        mel_acc = torch.zeros(base_mel.numel(), dtype=torch.float64, device=dev)
+        mel_prev = torch.zeros_like(mel_acc)
+        c_acc = torch.zeros(n * plan.coeff_numel, dtype=torch.float32, device=dev)
+        c_prev = torch.zeros_like(c_acc)
+        for k0, cnt in chunks(k_lo, k_hi, group):
+            img = plan.waverec(z, n, alphas=alphas[k0:k0 + cnt]).view(cnt * n, -1)
+            flat_scaled = None
+            g_mel, cg = self._grads_from_rec(plan, img, y, cnt, n)
+            weights = None
+            if shard.world > 1:
+                wk = np.array([0.0 if self.n_samples == 1 else (0.5 if k in (0, self.n_samples - 1) else 1.0)
+                               for k in range(k0, k0 + cnt)], dtype=np.float32)
+                weights = torch.from_numpy(wk).to(dev)
+            trapz_stream(g_mel, cnt, k0, mel_prev, mel_acc, weights)
+            for b in range(plan.nbands):
+                nb = int(np.prod(plan.band_shapes[b]))
+                lo, hi = n * plan.band_offsets[b], n * (plan.band_offsets[b] + nb)
+                src = cg[cnt * n * plan.band_offsets[b]:cnt * n * (plan.band_offsets[b] + nb)]
+                trapz_stream(src, cnt, k0, c_prev[lo:hi], c_acc[lo:hi], weights)
+            del flat_scaled
+        shard.all_reduce_sum(mel_acc)
+        shard.all_reduce_sum(c_acc)
+        mel = base_mel.cpu().numpy() * mel_acc.view(base_mel.shape).cpu().numpy()
+        prod = [b * i for b, i in zip(base_z, [v.cpu().numpy() for v in plan.split(c_acc, n)])]
+        self.melspecs = mel
+        self.grad_coeffs = prod
+        return mel, prod
+
+    def _grads_from_rec(self, plan, rec, y, groups, n):
+        rec_leaf = rec.detach().requires_grad_(True)
+        with torch.enable_grad():
+            mel = melspec_db(rec_leaf, self.n_fft, self.sample_rate, self.n_mels)
+        g_mel = input_gradient(self.model, mel.detach(), y, groups, n, self.autocast_dtype)
+        (g_rec,) = torch.autograd.grad(mel, rec_leaf, grad_outputs=g_mel)
+        return g_mel, plan.adjoint(g_rec.contiguous())
+
+    def __call__(self, x, y):
+        if self.method == "smooth":
+            return self.smooth_wam(x, y)
+        elif self.method == "integratedgrad":
+            return self.integrated_wam(x, y)

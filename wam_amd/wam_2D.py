@@ -1,0 +1,368 @@
+"""WAM for images on MI355X: drop-in for the reference's ``lib/wam_2D.py``.
+
+Same classes, constructor arguments, call signatures, return types and side attributes as
+``BaseWAM2D`` (lib/wam_2D.py:50-264) and ``WaveletAttribution2D`` (:343-536). What changes is
+where the work happens: every wavelet transform, its adjoint, the SmoothGrad noise, the IG path
+scaling, the per-subband channel-mean |.| with batch-global maxima and the mosaic accumulation
+run as HIP kernels (libwam_hip.so) on the model's GPU; several noise samples / IG steps are
+batched into one model forward/backward; nothing goes back to the host but the final map.
+
+Build-only keyword arguments (all optional, after the reference's own):
+  noise          'numpy' (default) = the reference's legacy np.random stream, bit-identical noise;
+                 'philox' = counter-based Philox4x32-10 generated on the GPU (fast path).
+  frame          'legacy' (default) = the reference's hard-coded 224 canvas, including its errors;
+                 'native' = canvas of the input's own size (runs db4 SmoothGrad at 224, IG at 512).
+  sample_batch   noise samples / IG steps per model call (default: as many as fit 256 images).
+  autocast_dtype e.g. torch.bfloat16: run the explained model under autocast (WAM stays fp32).
+  channels_last  feed the model NHWC tensors.
+  dist           True / ProcessGroup: shard samples (steps) over torch.distributed ranks and
+                 all-reduce the accumulated map (RCCL on ROCm); every rank returns the full map.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import frames
+from .constants import WaveletDetailTuple2d
+from .engine import Shard, auto_group, chunks, input_gradient, legacy_noise, model_device, require_gpu_device
+from .plan import frame_accumulate, frame_trapz, get_plan, item_sigma, noise_add, reproject_scales, subband_maps
+
+
+def _to_numpy_2d(plan, flat, batch_items, n, c, first_item=0):
+    views = plan.split(flat, batch_items)
+    out = []
+    for b, v in enumerate(views):
+        arr = v[first_item * c:(first_item + n) * c].reshape((n, c) + plan.band_shapes[b]).detach().cpu().numpy()
+        out.append(arr)
+    res = [out[0]]
+    for lv in range(plan.levels):
+        res.append(WaveletDetailTuple2d(out[1 + 3 * lv], out[2 + 3 * lv], out[3 + 3 * lv]))
+    return res
+
+
+def _bilinear_np(a, size):
+    t = torch.as_tensor(np.ascontiguousarray(a))[None, None]
+    return F.interpolate(t, size=(size, size), mode="bilinear", align_corners=False)[0, 0].numpy()
+
+
+class BaseWAM2D:
+    """Single gradient pass in the wavelet domain (lib/wam_2D.py:50-264)."""
+
+    def __init__(self, model, wavelet="haar", J=3, device=None, mode="reflect", approx_coeffs=False,
+                 normalize_coeffs=True, *, frame="legacy", autocast_dtype=None, channels_last=False):
+        self.wavelet = wavelet
+        self.J = J
+        self.mode = mode
+        self.approx_coeffs = approx_coeffs
+        self.normalize_coeffs = normalize_coeffs
+        if device is not None:
+            model = model.to(device)
+            self.model = model
+            self.device = device
+        else:
+            self.model = model
+            self.device = next(model.parameters()).device
+        self.frame = frame
+        self.autocast_dtype = autocast_dtype
+        self.channels_last = channels_last
+        self._pass = None
+        self._wavelet_coeffs = None
+        self._gradient_coeffs = None
+        self._scales = None
+
+    # ------------------------------------------------------------------ device helpers
+    @property
+    def _dev(self):
+        return require_gpu_device(model_device(self.model, self.device))
+
+    def _prep(self, x):
+        if not isinstance(x, torch.Tensor):
+            x = torch.as_tensor(np.asarray(x))
+        return x.detach().to(self._dev, dtype=torch.float32).contiguous()
+
+    # ------------------------------------------------------------------ lazy side attributes
+    def _record_pass(self, plan, coeff_flat, grad_flat, batch_items, first_item, n, c, coeff_items=None,
+                     coeff_first=None):
+        ci = batch_items if coeff_items is None else coeff_items
+        cf = first_item if coeff_first is None else coeff_first
+        self._pass = (plan, (coeff_flat, ci, cf), (grad_flat, batch_items, first_item), n, c)
+        self._wavelet_coeffs = None
+        self._gradient_coeffs = None
+        self._scales = None
+
+    @property
+    def wavelet_coeffs(self):
+        if self._wavelet_coeffs is None and self._pass is not None:
+            plan, (cf, b, f), _, n, c = self._pass
+            self._wavelet_coeffs = _to_numpy_2d(plan, cf, b, n, c, f)
+        return self._wavelet_coeffs
+
+    @wavelet_coeffs.setter
+    def wavelet_coeffs(self, v):
+        self._wavelet_coeffs = v
+
+    @property
+    def gradient_coeffs(self):
+        if self._gradient_coeffs is None and self._pass is not None:
+            plan, _, (gf, b, f), n, c = self._pass
+            self._gradient_coeffs = _to_numpy_2d(plan, gf, b, n, c, f)
+        return self._gradient_coeffs
+
+    @gradient_coeffs.setter
+    def gradient_coeffs(self, v):
+        self._gradient_coeffs = v
+
+    @property
+    def scales(self):
+        if self._scales is None and self._pass is not None:
+            self._scales = self.disentangle_scales(self.gradient_coeffs, approx_coeffs=self.approx_coeffs)
+        return self._scales
+
+    @scales.setter
+    def scales(self, v):
+        self._scales = v
+
+    # ------------------------------------------------------------------ reference API
+    def _coeff_plan(self, coeffs):
+        """Plan for an explicit coefficient list (image=False): the even spatial size whose
+        decomposition has these coefficient shapes (what ptwt.waverec2 reconstructs)."""
+        h1, w1 = coeffs[-1].horizontal.shape[-2:]
+        from .filters import get_wavelet
+        L = len(get_wavelet(self.wavelet).dec_lo)
+        shape = (2 * h1 + 2 - L, 2 * w1 + 2 - L)
+        plan = get_plan(2, shape, len(coeffs) - 1, self.wavelet, self.mode, self._dev)
+        want = [tuple(coeffs[0].shape[-2:])] + [tuple(t.shape[-2:]) for c in coeffs[1:] for t in c]
+        if want != [tuple(s) for s in plan.band_shapes]:
+            raise AssertionError("padding error, please check if dec and rec wavelets are identical.")
+        return plan
+
+    def __call__(self, x, y, image=True):
+        dev = self._dev
+        if image:
+            x = self._prep(x)
+            n, c, h, w = x.shape
+            plan = get_plan(2, (h, w), self.J, self.wavelet, self.mode, dev)
+            flat = plan.wavedec(x.view(n * c, h, w))
+        else:
+            coeffs = x
+            plan = self._coeff_plan(coeffs)
+            n, c = coeffs[0].shape[:2]
+            bands = [coeffs[0]] + [t for lv in coeffs[1:] for t in lv]
+            flat = torch.cat([b.detach().to(dev, torch.float32).reshape(-1) for b in bands])
+        img = plan.waverec(flat, n * c)[0].view((n, c) + plan.rec_shape)
+        g = input_gradient(self.model, img, y, 1, n, self.autocast_dtype, self.channels_last)
+        cg = plan.adjoint(g.view((n * c,) + plan.rec_shape))
+        self._record_pass(plan, flat, cg, n * c, 0, n, c)
+        maps, bmax = subband_maps(plan, cg, 1, n, c)
+        if self.frame == "native":
+            canvas, base = plan.shape, plan.shape
+        else:
+            r = 2 * plan.band_shapes[-1][1]
+            canvas, base = (r, r), (224, 224)
+        gmap = frames.mosaic_map(plan, canvas, base, dev)
+        frame = torch.zeros(n * canvas[0] * canvas[1], dtype=torch.float64, device=dev)
+        frame_accumulate(1, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, frame)
+        return frame.view(n, canvas[0], canvas[1]).cpu().numpy()
+
+    def disentangle_scales(self, coeffs, approx_coeffs=False):
+        """lib/wam_2D.py:133-198 (per-sample side attribute; evaluated lazily on access)."""
+        batch_size = coeffs[0].shape[0]
+        img_size = int(2 * coeffs[-1].horizontal.shape[-1])
+        num_levels = self.J
+        vis = np.zeros((batch_size, num_levels + 1 if approx_coeffs else num_levels, img_size, img_size))
+        img_batch = 0
+        for i, coeff in enumerate(coeffs[1:][::-1]):
+            hz = np.abs(coeff.horizontal.mean(axis=1))
+            hz /= hz.max()
+            dg = np.abs(coeff.diagonal.mean(axis=1))
+            dg /= dg.max()
+            vt = np.abs(coeff.vertical.mean(axis=1))
+            vt /= vt.max()
+            for img_batch in range(batch_size):
+                vis[img_batch, i] = (_bilinear_np(vt[img_batch], img_size) + _bilinear_np(dg[img_batch], img_size) +
+                                     _bilinear_np(hz[img_batch], img_size))
+        if approx_coeffs:
+            ap = np.abs(coeffs[0].mean(axis=1))
+            ap /= ap.max()
+            vis[img_batch, num_levels] = _bilinear_np(ap[img_batch], img_size)  # reference: stale img_batch
+        return vis
+
+    def visualize_grad_wam(self, coeffs):
+        """lib/wam_2D.py:200-264 on host coefficient gradients (numpy lists)."""
+        batch = coeffs[0].shape[0]
+        size = int(2 * coeffs[-1].horizontal.shape[-1])
+        vis = np.zeros((batch, size, size))
+        ap = np.abs(coeffs[0].mean(axis=1))
+        if self.normalize_coeffs:
+            ap /= ap.max()
+        vis[:, :ap.shape[1], :ap.shape[2]] = ap
+        for i, coeff in enumerate(coeffs[1:][::-1]):
+            e, s = int(224 / 2 ** i), int(224 / 2 ** (i + 1))
+            hz = np.abs(coeff.horizontal.mean(axis=1))
+            vt = np.abs(coeff.vertical.mean(axis=1))
+            dg = np.abs(coeff.diagonal.mean(axis=1))
+            if self.normalize_coeffs:
+                hz /= hz.max()
+                dg /= dg.max()
+                vt /= vt.max()
+            vis[:, s:e, s:e] = dg[:, :(e - s), :(e - s)]
+            vis[:, s:e, :s] = vt[:, :(e - s), :(e - s)]
+            vis[:, :s, s:e] = hz[:, :(e - s), :(e - s)]
+        return vis
+
+
+class WaveletAttribution2D(BaseWAM2D):
+    """SmoothGrad / Integrated-Gradients WAM (lib/wam_2D.py:343-536)."""
+
+    def __init__(self, model, wavelet="haar", method="smooth", J=3, device=None, mode="reflect", approx_coeffs=False,
+                 normalize_coeffs=True, n_samples=25, stdev_spread=0.25, random_seed=42, *, noise="numpy",
+                 frame="legacy", sample_batch=None, autocast_dtype=None, channels_last=False, dist=None):
+        super().__init__(model, wavelet=wavelet, J=J, device=device, mode=mode, approx_coeffs=approx_coeffs,
+                         normalize_coeffs=normalize_coeffs, frame=frame, autocast_dtype=autocast_dtype,
+                         channels_last=channels_last)
+        self.method = method
+        self.n_samples = n_samples
+        self.stdev_spread = stdev_spread
+        self.random_seed = random_seed
+        if noise not in ("numpy", "philox"):
+            raise ValueError("noise must be 'numpy' or 'philox'")
+        self.noise = noise
+        self.sample_batch = sample_batch
+        self.dist = dist
+        self.wam = BaseWAM2D(model, wavelet=wavelet, J=J, mode=mode, device=device, approx_coeffs=approx_coeffs,
+                             normalize_coeffs=normalize_coeffs, frame=frame, autocast_dtype=autocast_dtype,
+                             channels_last=channels_last)
+        self._avg_dev = None
+
+    # ------------------------------------------------------------------ .scales (lazy)
+    @property
+    def scales(self):
+        if self._scales is None and self._avg_dev is not None:
+            self._scales = self._reproject_dev(self._avg_dev, self.J, self.approx_coeffs)
+        return self._scales
+
+    @scales.setter
+    def scales(self, v):
+        self._scales = v
+
+    def _set_result(self, avg_dev):
+        self._avg_dev = avg_dev
+        self._scales = None
+
+    # ------------------------------------------------------------------ estimators
+    def smooth_gradcam(self, x, y):
+        """lib/wam_2D.py:379-415."""
+        dev = self._dev
+        x = self._prep(x)
+        n, c, h, w = x.shape
+        plan = get_plan(2, (h, w), self.J, self.wavelet, self.mode, dev)
+        gmap, (rh, rw) = frames.smooth_frame(plan, n, self.frame, dev)
+        item = c * h * w
+        sigma = item_sigma(x, item, item, self.stdev_spread)
+        shard = Shard(self.dist)
+        s_lo, s_hi = shard.range(self.n_samples)
+        group = auto_group(self.model, n, self.sample_batch)
+        frame = torch.zeros(n * rh * rw, dtype=torch.float64, device=dev)
+        noise_it = None
+        if self.noise == "numpy":
+            noise_it = legacy_noise([float(v) for v in sigma.cpu().numpy()], (c, h, w), self.random_seed,
+                                    list(range(s_lo, s_hi)))
+        rec = plan.rec_shape
+        last = None
+        for s0, cnt in chunks(s_lo, s_hi, group):
+            host = None
+            if noise_it is not None:
+                arr = np.stack([next(noise_it)[1] for _ in range(cnt)])
+                host = torch.from_numpy(arr).pin_memory().to(dev, non_blocking=True)
+            noisy = noise_add(x, sigma, cnt, n, item, item, seed=self.random_seed, sample_base=s0, host_noise=host)
+            flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
+            img = plan.waverec(flat, cnt * n * c)[0].view((cnt * n, c) + rec)
+            g = input_gradient(self.model, img, y, cnt, n, self.autocast_dtype, self.channels_last)
+            cg = plan.adjoint(g.view((cnt * n * c,) + rec))
+            maps, bmax = subband_maps(plan, cg, cnt, n, c)
+            frame_accumulate(cnt, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, frame)
+            last = (plan, flat, cg, cnt * n * c, (cnt - 1) * n, n, c)
+        if last is not None:
+            self.wam._record_pass(*last)
+        shard.all_reduce_sum(frame)
+        avg = frame.view(n, rh, rw) / self.n_samples
+        self._set_result(avg)
+        return avg.cpu().numpy()
+
+    def intergrated_wam(self, x, y):
+        """lib/wam_2D.py:417-459 (trapezoid over alpha = linspace(0, 1, n_samples), dx = 1)."""
+        dev = self._dev
+        x = self._prep(x)
+        n, c, h, w = x.shape
+        plan = get_plan(2, (h, w), self.J, self.wavelet, self.mode, dev)
+        bmap, gmap, (rh, rw) = frames.ig_frames(plan, n, self.frame, dev)
+        z = plan.wavedec(x.view(n * c, h, w))
+        zmaps, zmax = subband_maps(plan, z, 1, n, c)
+        base = torch.zeros(n * rh * rw, dtype=torch.float64, device=dev)
+        frame_accumulate(1, n, bmap, zmaps, plan.coeff_numel, zmax, plan.nbands, True, base)
+        alphas = np.linspace(0, 1, self.n_samples)
+        shard = Shard(self.dist)
+        k_lo, k_hi = shard.range(self.n_samples)
+        group = auto_group(self.model, n, self.sample_batch)
+        acc = torch.zeros(n * rh * rw, dtype=torch.float32, device=dev)
+        prev = torch.zeros_like(acc)
+        rec = plan.rec_shape
+        last = None
+        for k0, cnt in chunks(k_lo, k_hi, group):
+            img = plan.waverec(z, n * c, alphas=alphas[k0:k0 + cnt]).view((cnt * n, c) + rec)
+            g = input_gradient(self.model, img, y, cnt, n, self.autocast_dtype, self.channels_last)
+            cg = plan.adjoint(g.view((cnt * n * c,) + rec))
+            maps, bmax = subband_maps(plan, cg, cnt, n, c)
+            weights = None
+            if shard.world > 1:
+                wk = np.ones(cnt, dtype=np.float32)
+                for i in range(cnt):
+                    k = k0 + i
+                    wk[i] = 0.0 if self.n_samples == 1 else (0.5 if k in (0, self.n_samples - 1) else 1.0)
+                weights = torch.from_numpy(wk).to(dev)
+            frame_trapz(cnt, k0, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, prev, acc,
+                        weights)
+            last = (plan, None, cg, cnt * n * c, (cnt - 1) * n, n, c, float(alphas[k0 + cnt - 1]))
+        if last is not None:
+            plan_, _, cg, b, f, nn, cc, alpha = last
+            coeff = z * float(np.float32(alpha))  # the path coefficients alpha * z of the last step
+            self.wam._record_pass(plan_, coeff, cg, b, f, nn, cc, coeff_items=n * c, coeff_first=0)
+        shard.all_reduce_sum(acc)
+        out = base.view(n, rh, rw) * acc.view(n, rh, rw).double()
+        self._set_result(out)
+        return out.cpu().numpy()
+
+    def alter(self, alpha, coeffs):
+        """lib/wam_2D.py:461-476."""
+        altered = [coeffs[0] * alpha]
+        for coeff in coeffs[1:]:
+            altered.append(WaveletDetailTuple2d(coeff.horizontal * alpha, coeff.vertical * alpha,
+                                                coeff.diagonal * alpha))
+        return altered
+
+    def __call__(self, x, y):
+        if self.method == "smooth":
+            return self.smooth_gradcam(x, y)
+        if self.method == "integratedgrad":
+            return self.intergrated_wam(x, y)
+        return None
+
+    # ------------------------------------------------------------------ reprojection
+    def _reproject_dev(self, avg_dev, num_levels, approx_coeffs):
+        n, size = avg_dev.shape[0], avg_dev.shape[1]
+        if avg_dev.shape[2] != size:
+            raise NotImplementedError("reproject_wam on a non-square map")
+        sc = reproject_scales(avg_dev.contiguous(), self.J, approx_coeffs).cpu().numpy()
+        out = np.zeros((n, num_levels + 1 if approx_coeffs else num_levels, size, size))
+        for j in range(self.J):
+            if j >= out.shape[1]:
+                raise IndexError("index %d is out of bounds for axis 1 with size %d" % (j, out.shape[1]))
+            out[:, j] = sc[:, j]
+        if approx_coeffs:
+            out[:, num_levels] = sc[:, self.J]
+        return out
+
+    def reproject_wam(self, average_gradients, num_levels, approx_coeffs=False):
+        """lib/wam_2D.py:488-536 (cv2 INTER_LINEAR reprojection as a HIP kernel)."""
+        avg = torch.as_tensor(np.asarray(average_gradients, dtype=np.float64)).to(self._dev)
+        return self._reproject_dev(avg, num_levels, approx_coeffs)
