@@ -178,10 +178,11 @@ def waverecn(coeffs, wavelet, ndim):
 
 
 def adjointn(grad, coeff_shapes_like, wavelet, ndim):
-    """VJP of waverecn w.r.t. its coefficients: zero-mode analysis with reverse(rec) filters."""
+    """VJP of waverecn w.r.t. its coefficients: zero-mode analysis with reverse(rec) filters.
+    coeff_shapes_like: the number of levels, or a coefficient list of that depth."""
     _, _, rec_lo, rec_hi = filter_bank(wavelet) if isinstance(wavelet, str) else wavelet
     fb = (rec_lo[::-1], rec_hi[::-1], rec_lo, rec_hi)
-    level = len(coeff_shapes_like) - 1
+    level = coeff_shapes_like if isinstance(coeff_shapes_like, int) else len(coeff_shapes_like) - 1
     out = []
     g = np.asarray(grad, dtype=np.float64)
     for _ in range(level):

@@ -1,0 +1,96 @@
+"""Multi-process (world_size 2, gloo, CPU) coverage of the sharded path.
+
+Each rank runs wam_amd.engine's sharding (Shard.range over noise samples / IG steps, the numpy
+noise stream positioned for its slice, ig_weights / legacy3d_weights) with the oracle standing
+in for the per-sample GPU pass, then all-reduces its partial accumulator exactly like the
+classes do (Shard.all_reduce_sum). The combined result must equal the single-process reference.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import testmodels
+        from oracle import wam_ref
+        from wam_amd import engine
+
+        shard = engine.Shard(True)
+        assert (shard.rank, shard.world) == (rank, world)
+        res = {}
+        # --- 2D SmoothGrad: samples sharded, per-sample max stays local, SUM of mosaics
+        rs = np.random.RandomState(0)
+        x = torch.tensor(rs.standard_normal((2, 3, 224, 224)).astype(np.float32))
+        model = testmodels.TinySmooth2D()
+        n = 5
+        lo, hi = shard.range(n)
+        sig = [float(np.float32(0.25) * (x[i].max() - x[i].min())) for i in range(2)]
+        acc = torch.zeros(2, 224, 224, dtype=torch.float64)
+        for s, noise in engine.legacy_noise(sig, (3, 224, 224), 42, list(range(lo, hi))):
+            noisy = x + torch.tensor(noise)
+            _, g = wam_ref.single_pass_2d(model, noisy, [1, 2], "haar", 3, "reflect")
+            acc += torch.tensor(wam_ref.mosaic_2d(g, True, (224, 224), (224, 224)))
+        shard.all_reduce_sum(acc)
+        res["smooth"] = (acc / n).numpy()
+        # --- IG weighted form over sharded steps
+        G = torch.tensor(np.random.RandomState(1).standard_normal((7, 50)).astype(np.float32))
+        k0, k1 = shard.range(7)
+        w = torch.tensor(engine.ig_weights(k0, k1 - k0, 7))
+        part = (w[:, None] * G[k0:k1]).sum(0)
+        shard.all_reduce_sum(part)
+        res["ig"] = part.numpy()
+        # --- legacy 3D averaging weights over sharded samples
+        C = G.abs()
+        s0, s1 = shard.range(7)
+        w3 = torch.tensor(engine.legacy3d_weights(s0, s1 - s0, 7))
+        part3 = (w3[:, None] * C[s0:s1]).sum(0)
+        shard.all_reduce_sum(part3)
+        res["cube"] = part3.numpy()
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_sharding_matches_single_process():
+    from oracle import wam_ref
+    import testmodels
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=600) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rs = np.random.RandomState(0)
+    x = torch.tensor(rs.standard_normal((2, 3, 224, 224)).astype(np.float32))
+    ref = wam_ref.smooth_2d(testmodels.TinySmooth2D(), x, [1, 2], wavelet="haar", J=3, n_samples=5)
+    G = np.random.RandomState(1).standard_normal((7, 50)).astype(np.float32)
+    avg = np.zeros(50, dtype=np.float32)
+    for s in range(7):
+        avg = (avg + np.abs(G[s])) / np.float32(7)
+    for r in range(world):
+        assert np.abs(out[r]["smooth"] - ref).max() < 1e-12   # same per-sample maps, fp64 sums
+        assert np.allclose(out[r]["ig"], np.trapz(G, axis=0), rtol=1e-5, atol=1e-6)
+        assert np.allclose(out[r]["cube"], avg, rtol=1e-5, atol=1e-30)
+        assert np.array_equal(out[0]["smooth"], out[r]["smooth"])

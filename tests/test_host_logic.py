@@ -1,0 +1,140 @@
+"""Host-side logic of wam_amd on the CPU: mosaic / cube gather maps vs the reference's slice
+assignments, loss seed gradients vs autograd of diag(out[:, y]).mean(), the numpy noise stream,
+sample/step sharding and the sharded-accumulation weights."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dwt, wam_ref
+from wam_amd import engine, frames
+
+
+class FakePlan:
+    """Band layout of a plan without a device (sizes from the oracle's level rules)."""
+
+    def __init__(self, ndim, shape, J, wavelet):
+        L = len(dwt.filter_bank(wavelet)[0])
+        per_axis = [dwt.level_sizes(n, L, J) for n in shape]
+        self.ndim, self.shape, self.levels = ndim, tuple(shape), J
+        per = (1 << ndim) - 1
+        self.band_shapes = [tuple(a[J - 1] for a in per_axis)]
+        for lv in range(J - 1, -1, -1):
+            self.band_shapes += [tuple(a[lv] for a in per_axis)] * per
+        self.band_offsets = [0]
+        for s in self.band_shapes:
+            self.band_offsets.append(self.band_offsets[-1] + int(np.prod(s)))
+        self.coeff_numel = self.band_offsets[-1]
+        self.nbands = len(self.band_shapes)
+
+    def __hash__(self):
+        return hash((self.ndim, self.shape, self.levels, tuple(self.band_shapes)))
+
+
+def _apply(gmap_src, gmap_band, maps_item, bmax, normalize):
+    src = gmap_src.numpy()
+    band = gmap_band.numpy()
+    out = np.zeros(src.shape, dtype=np.float64)
+    ok = src >= 0
+    v = maps_item[src[ok]]
+    if normalize:
+        v = v / bmax[band[ok]]
+    out[ok] = v
+    return out
+
+
+@pytest.mark.parametrize("wav,size,J,frame", [("haar", 224, 3, "legacy"), ("db4", 224, 3, "native"),
+                                              ("sym8", 96, 2, "native"), ("haar", 224, 5, "legacy"),
+                                              ("db6", 104, 3, "native")])
+def test_mosaic_gather_map_matches_reference_assignments(wav, size, J, frame):
+    rs = np.random.RandomState(0)
+    p = FakePlan(2, (size, size), J, wav)
+    n = 2
+    bands = [np.abs(rs.standard_normal((n,) + s)).astype(np.float32) for s in p.band_shapes]
+    # oracle container order = ptwt band order: [A_J, (H,V,D)_J, ..., (H,V,D)_1]
+    grads = [bands[0][:, None]] + [tuple(bands[1 + 3 * i + k][:, None] for k in range(3)) for i in range(J)]
+    (src, band), (rh, rw) = frames.smooth_frame(p, n, frame, "cpu")
+    canvas, base = wam_ref.frame_geometry(frame, size, size, p.band_shapes[-1][1])
+    ref = wam_ref.mosaic_2d(grads, True, canvas, base)
+    bmax = np.array([b.max() for b in bands], dtype=np.float32)
+    for i in range(n):
+        packed = np.concatenate([b[i].reshape(-1) for b in bands])
+        got = _apply(src, band, packed, bmax, True).reshape(rh, rw)
+        assert np.array_equal(got, ref[i])
+
+
+def test_legacy_frame_errors():
+    with pytest.raises(ValueError):
+        frames.smooth_frame(FakePlan(2, (224, 224), 3, "db4"), 1, "legacy", "cpu")  # 230 canvas
+    with pytest.raises(ValueError):
+        frames.ig_frames(FakePlan(2, (128, 128), 3, "haar"), 1, "legacy", "cpu")   # IG is 224-only
+    with pytest.raises(ValueError):
+        frames.smooth_frame(FakePlan(2, (224, 224), 6, "haar"), 1, "legacy", "cpu")  # J >= 6
+    frames.ig_frames(FakePlan(2, (224, 224), 3, "sym8"), 1, "legacy", "cpu")        # runs in the reference
+
+
+def test_cube_map_matches_refactor():
+    rs = np.random.RandomState(1)
+    p = FakePlan(3, (16, 16, 16), 2, "haar")
+    bands = [rs.standard_normal(s).astype(np.float32) for s in p.band_shapes]
+    keys = ["aad", "ada", "add", "daa", "dad", "dda", "ddd"]
+    c = [bands[0]] + [{k: bands[1 + 7 * i + j] for j, k in enumerate(keys)} for i in range(2)]
+    ref = wam_ref.refactor_3d([c], 2, 16)[0]
+    src = frames.cube_map(p, 16, "cpu").numpy()
+    packed = np.abs(np.concatenate([b.reshape(-1) for b in bands]))
+    assert (src >= 0).all()
+    assert np.array_equal(packed[src].reshape(16, 16, 16), ref)
+
+
+@pytest.mark.parametrize("y,n", [(3, 4), ([1, 5, 2, 2], 4), (torch.tensor([0, 1, 2]), 3), ([4, 5], 3), (7, 1)])
+def test_seed_gradient_matches_autograd_of_reference_loss(y, n):
+    groups = 3
+    out = torch.randn(groups * n, 10, requires_grad=True)
+    loss = sum(torch.diag(out[s * n:(s + 1) * n][:, y]).mean() for s in range(groups))
+    (g_ref,) = torch.autograd.grad(loss, out)
+    g = engine.seed_gradient(out.detach(), y, groups, n)
+    assert torch.equal(g, g_ref)
+
+
+def test_legacy_noise_stream_matches_reference_loop():
+    x = torch.tensor(np.random.RandomState(3).standard_normal((3, 2, 5, 5)).astype(np.float32))
+    sig = [float(0.25 * (x[i].max() - x[i].min())) for i in range(3)]
+    ref = [noisy for _, noisy in wam_ref.legacy_noise_stream(x, 4, 0.25, 42)]
+    got = dict(engine.legacy_noise(sig, (2, 5, 5), 42, [1, 3]))
+    for s in (1, 3):
+        assert np.array_equal((x + torch.tensor(got[s])).numpy(), ref[s].numpy())
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("n", [1, 3, 25, 64])
+def test_shard_ranges_partition(world, n):
+    seen = []
+    for r in range(world):
+        s = engine.Shard.__new__(engine.Shard)
+        s.group, s.rank, s.world = None, r, world
+        lo, hi = s.range(n)
+        seen.extend(range(lo, hi))
+        assert hi - lo in (n // world, n // world + 1)
+    assert seen == list(range(n))
+
+
+def test_sharded_weights_reproduce_sequential_forms():
+    rs = np.random.RandomState(5)
+    for n in (1, 2, 5, 25):
+        G = rs.standard_normal((n, 7)).astype(np.float32)
+        ref = np.trapz(G, axis=0)
+        w = np.concatenate([engine.ig_weights(k0, c, n) for k0, c in engine.chunks(0, n, 3)])
+        assert np.allclose((w[:, None] * G).sum(0), ref, rtol=1e-5, atol=1e-6)
+        cube = np.abs(G)
+        avg = np.zeros(7, dtype=np.float32)
+        for s in range(n):
+            avg = (avg + cube[s]) / np.float32(n)
+        w3 = engine.legacy3d_weights(0, n, n)
+        assert np.allclose((w3[:, None] * cube).sum(0), avg, rtol=1e-5, atol=1e-30)
+
+
+def test_auto_group():
+    m = torch.nn.Linear(2, 2).eval()
+    assert engine.auto_group(m, 64, None) == 4
+    assert engine.auto_group(m, 1, None) == 256
+    assert engine.auto_group(m.train(), 64, None) == 1
+    assert engine.auto_group(m, 64, 3) == 3

@@ -1,0 +1,103 @@
+"""The oracle is pinned before it is trusted (CPU only).
+
+* oracle/dwt.py and oracle/ptwt_torch.py vs PyWavelets 1.1.1 known answers (1D/2D/3D, five modes,
+  even and odd sizes, analysis AND synthesis of random coefficients) and vs the MATLAB R2012a
+  single-level answers shipped in pywt's test data;
+* the adjoint identity (autograd through the ptwt restatement == zero-mode reverse(rec) analysis);
+* oracle/wam_ref.py vs the outputs of the REFERENCE's own lib/wam_{1,2,3}D.py
+  (tests/golden/glue_goldens.npz).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dwt, ptwt_torch, wam_ref
+from tests.golden.glue_cases import CASES, make_inputs, make_model
+from tests.helpers import flat_bands, max_rel, npz, pywt_cases, pywt_coeffs
+
+
+@pytest.mark.parametrize("dim", [1, 2, 3])
+def test_numpy_oracle_vs_pywt(dim):
+    d = npz("pywt_dwt.npz")
+    fn = {1: (dwt.wavedec, dwt.waverec), 2: (dwt.wavedec2, dwt.waverec2), 3: (dwt.wavedec3, dwt.waverec3)}[dim]
+    for case, wav, mode, J in pywt_cases(dim):
+        got = flat_bands(fn[0](d[case + "_x"], wav, J, mode), dim)
+        ref = flat_bands(pywt_coeffs(case, dim, J), dim)
+        for g, r in zip(got, ref):
+            assert g.shape == r.shape and np.abs(g - r).max() < 1e-10, (case, wav, mode)
+        rec = fn[1](pywt_coeffs(case, dim, J, prefix="r"), wav)
+        assert rec.shape == d[case + "_rrec"].shape
+        assert np.abs(rec - d[case + "_rrec"]).max() < 1e-10, (case, wav, mode)
+        rt = fn[1](pywt_coeffs(case, dim, J), wav)
+        assert np.abs(rt - d[case + "_rec"]).max() < 1e-10
+
+
+@pytest.mark.parametrize("dim", [1, 2, 3])
+def test_torch_oracle_vs_pywt(dim):
+    d = npz("pywt_dwt.npz")
+    dec = {1: ptwt_torch.wavedec, 2: ptwt_torch.wavedec2, 3: ptwt_torch.wavedec3}[dim]
+    for case, wav, mode, J in pywt_cases(dim)[::2]:
+        got = flat_bands(dec(torch.tensor(d[case + "_x"]), wav, level=J, mode=mode), dim)
+        ref = flat_bands(pywt_coeffs(case, dim, J), dim)
+        for g, r in zip(got, ref):
+            assert tuple(g.shape) == r.shape and np.abs(g.numpy() - r).max() < 1e-10, (case, wav, mode)
+
+
+def test_oracle_vs_matlab():
+    d = npz("matlab_dwt.npz")
+    for c in sorted({k.rsplit("_", 1)[0] for k in d.files}):
+        mode, wav, n = c.split("_")
+        lo, hi = dwt.analysis_axis(d[c + "_x"], *dwt.filter_bank(wav)[:2], -1, mode)
+        assert max_rel(lo, d[c + "_ma"]) < 1e-5 and max_rel(hi, d[c + "_md"]) < 1e-5, c
+
+
+@pytest.mark.parametrize("wav", ["haar", "db4", "sym8", "bior2.2"])
+@pytest.mark.parametrize("shape", [(2, 3, 40, 40), (1, 2, 45, 37)])
+def test_adjoint_identity(wav, shape):
+    """A.4: d waverec2 / d coeffs == zero-mode analysis with reverse(rec) filters, exactly."""
+    x = torch.randn(*shape, dtype=torch.float64)
+    cs = ptwt_torch.wavedec2(x, wav, level=3, mode="reflect")
+    leaves = [cs[0].requires_grad_()] + [ptwt_torch.WaveletDetailTuple2d(*[t.requires_grad_() for t in c])
+                                         for c in cs[1:]]
+    img = ptwt_torch.waverec2(leaves, wav)
+    g = torch.randn_like(img)
+    img.backward(g)
+    adj = dwt.adjoint2(g.numpy(), 3, wav)
+    got = flat_bands(adj, 2)
+    ref = [t.grad.numpy() for t in flat_bands(leaves, 2)]
+    for a, b in zip(got, ref):
+        assert np.abs(a - b).max() < 1e-12
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_glue_oracle_vs_reference_goldens(name):
+    case = CASES[name]
+    g = npz("glue_goldens.npz")
+    x, y = make_inputs(case)
+    m = make_model(case)
+    kw = dict(case["kw"])
+    method = kw.pop("method")
+    if case["dim"] == 2:
+        approx = kw.pop("approx_coeffs", False)
+        r = (wam_ref.smooth_2d if method == "smooth" else wam_ref.ig_2d)(m, x, y, **kw)
+        assert np.abs(r - g[name]).max() < 1e-9
+        if case.get("scales"):
+            assert np.abs(wam_ref.reproject_wam(r, kw["J"], approx) - g[name + "_scales"]).max() < 1e-6
+    elif case["dim"] == 1:
+        mel, cs = (wam_ref.smooth_1d if method == "smooth" else wam_ref.ig_1d)(m, x, y, **kw)
+        assert max_rel(mel, g[name + "_mel"]) < 1e-6
+        for j, c in enumerate(cs):
+            assert max_rel(c, g[name + "_c%d" % j]) < 1e-6
+    else:
+        r = (wam_ref.smooth_3d if method == "smooth" else wam_ref.ig_3d)(m, x, y, **kw)
+        assert max_rel(r, g[name]) < 1e-6
+
+
+def test_level_sizes_match_survey():
+    """SURVEY.md section 8 coefficient sizes per config (pywt-verified there)."""
+    L = lambda w: len(dwt.filter_bank(w)[0])
+    assert dwt.level_sizes(224, L("haar"), 3) == [112, 56, 28]
+    assert dwt.level_sizes(224, L("db4"), 3) == [115, 61, 34]
+    assert dwt.level_sizes(80000, L("db6"), 5) == [40005, 20008, 10009, 5010, 2510]
+    assert dwt.level_sizes(512, L("sym8"), 5) == [263, 139, 77, 46, 30]
+    assert dwt.level_sizes(128, L("haar"), 2) == [64, 32]

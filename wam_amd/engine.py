@@ -124,6 +124,20 @@ class Shard:
         return t
 
 
+def ig_weights(k0, cnt, n):
+    """Trapezoid weights (dx = 1) of path steps k0..k0+cnt-1 out of n, for the sharded form
+    acc = sum_k w_k G_k (== np.trapz up to fp32 summation order)."""
+    if n == 1:
+        return np.zeros(cnt, dtype=np.float32)
+    return np.array([0.5 if k in (0, n - 1) else 1.0 for k in range(k0, k0 + cnt)], dtype=np.float32)
+
+
+def legacy3d_weights(s0, cnt, n):
+    """Weights of the reference's in-loop 3D averaging (lib/wam_3D.py:582-587):
+    avg_{s+1} = (avg_s + cube_s) / n  =>  avg_n = sum_s cube_s * n^-(n-s)."""
+    return np.array([float(n) ** (-(n - s)) for s in range(s0, s0 + cnt)], dtype=np.float32)
+
+
 def chunks(start, stop, size):
     out = []
     s = start

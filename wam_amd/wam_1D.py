@@ -11,7 +11,8 @@ sample_batch, autocast_dtype, dist).
 import numpy as np
 import torch
 
-from .engine import Shard, auto_group, chunks, input_gradient, legacy_noise, model_device, require_gpu_device
+from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, legacy_noise, model_device,
+                     require_gpu_device)
 from .melspec import melspec_db
 from .plan import accumulate_f32, get_plan, item_sigma, noise_add, trapz_stream
 
@@ -79,14 +80,15 @@ class BaseWAM1D:
     # ------------------------------------------------------------------ core pass (batched groups)
     def _grads(self, plan, flat, items, y, groups, n):
         """waverec -> melspec -> model -> (melspec grad [items,1,T,M], coefficient grads flat)."""
-        rec = plan.waverec(flat, items)[0]
+        return self._grads_from_rec(plan, plan.waverec(flat, items)[0], y, groups, n)
+
+    def _grads_from_rec(self, plan, rec, y, groups, n):
         rec_leaf = rec.detach().requires_grad_(True)
         with torch.enable_grad():
             mel = melspec_db(rec_leaf, self.n_fft, self.sample_rate, self.n_mels)
         g_mel = input_gradient(self.model, mel.detach(), y, groups, n, self.autocast_dtype)
         (g_rec,) = torch.autograd.grad(mel, rec_leaf, grad_outputs=g_mel)
-        cg = plan.adjoint(g_rec.contiguous())
-        return g_mel, cg
+        return g_mel, plan.adjoint(g_rec.contiguous())
 
     def compute_melspec(self, reconstruction, n_fft=1024, sample_rate=44100, n_mels=128):
         """lib/wam_1D.py:194-219: [N, W] -> [N, 1, T, n_mels] (on the GPU)."""
@@ -219,20 +221,16 @@ class WaveletAttribution1D(BaseWAM1D):
         c_prev = torch.zeros_like(c_acc)
         for k0, cnt in chunks(k_lo, k_hi, group):
             img = plan.waverec(z, n, alphas=alphas[k0:k0 + cnt]).view(cnt * n, -1)
-            flat_scaled = None
             g_mel, cg = self._grads_from_rec(plan, img, y, cnt, n)
             weights = None
             if shard.world > 1:
-                wk = np.array([0.0 if self.n_samples == 1 else (0.5 if k in (0, self.n_samples - 1) else 1.0)
-                               for k in range(k0, k0 + cnt)], dtype=np.float32)
-                weights = torch.from_numpy(wk).to(dev)
+                weights = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
             trapz_stream(g_mel, cnt, k0, mel_prev, mel_acc, weights)
             for b in range(plan.nbands):
                 nb = int(np.prod(plan.band_shapes[b]))
                 lo, hi = n * plan.band_offsets[b], n * (plan.band_offsets[b] + nb)
                 src = cg[cnt * n * plan.band_offsets[b]:cnt * n * (plan.band_offsets[b] + nb)]
                 trapz_stream(src, cnt, k0, c_prev[lo:hi], c_acc[lo:hi], weights)
-            del flat_scaled
         shard.all_reduce_sum(mel_acc)
         shard.all_reduce_sum(c_acc)
         mel = base_mel.cpu().numpy() * mel_acc.view(base_mel.shape).cpu().numpy()
@@ -240,14 +238,6 @@ class WaveletAttribution1D(BaseWAM1D):
         self.melspecs = mel
         self.grad_coeffs = prod
         return mel, prod
-
-    def _grads_from_rec(self, plan, rec, y, groups, n):
-        rec_leaf = rec.detach().requires_grad_(True)
-        with torch.enable_grad():
-            mel = melspec_db(rec_leaf, self.n_fft, self.sample_rate, self.n_mels)
-        g_mel = input_gradient(self.model, mel.detach(), y, groups, n, self.autocast_dtype)
-        (g_rec,) = torch.autograd.grad(mel, rec_leaf, grad_outputs=g_mel)
-        return g_mel, plan.adjoint(g_rec.contiguous())
 
     def __call__(self, x, y):
         if self.method == "smooth":

@@ -24,7 +24,8 @@ import torch.nn.functional as F
 
 from . import frames
 from .constants import WaveletDetailTuple2d
-from .engine import Shard, auto_group, chunks, input_gradient, legacy_noise, model_device, require_gpu_device
+from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, legacy_noise, model_device,
+                     require_gpu_device)
 from .plan import frame_accumulate, frame_trapz, get_plan, item_sigma, noise_add, reproject_scales, subband_maps
 
 
@@ -315,11 +316,7 @@ class WaveletAttribution2D(BaseWAM2D):
             maps, bmax = subband_maps(plan, cg, cnt, n, c)
             weights = None
             if shard.world > 1:
-                wk = np.ones(cnt, dtype=np.float32)
-                for i in range(cnt):
-                    k = k0 + i
-                    wk[i] = 0.0 if self.n_samples == 1 else (0.5 if k in (0, self.n_samples - 1) else 1.0)
-                weights = torch.from_numpy(wk).to(dev)
+                weights = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
             frame_trapz(cnt, k0, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, prev, acc,
                         weights)
             last = (plan, None, cg, cnt * n * c, (cnt - 1) * n, n, c, float(alphas[k0 + cnt - 1]))

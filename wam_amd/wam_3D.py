@@ -15,7 +15,8 @@ import torch
 
 from . import frames
 from .constants import KEYS3
-from .engine import Shard, auto_group, chunks, input_gradient, legacy_noise, model_device, require_gpu_device
+from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, legacy3d_weights, legacy_noise,
+                     model_device, require_gpu_device)
 from .plan import cube_accumulate, get_plan, item_sigma, noise_add, subband_maps
 
 
@@ -213,8 +214,8 @@ class WaveletAttribution3D(BaseWAM3D):
             if shard.world == 1:
                 self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 0, n_total=float(ns))
             else:
-                w = np.array([float(ns) ** (-(ns - s)) for s in range(s0, s0 + cnt)], dtype=np.float32)
-                self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 1, weights=torch.from_numpy(w).to(dev))
+                w = torch.from_numpy(legacy3d_weights(s0, cnt, ns)).to(dev)
+                self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 1, weights=w)
             self.wam._coeffs_src = (plan, flat, cnt * n * c, (cnt - 1) * n, n, c)
             self.wam._coeffs = None
         shard.all_reduce_sum(acc)
@@ -261,7 +262,6 @@ class WaveletAttribution3D(BaseWAM3D):
         acc = torch.zeros(n * S ** 3, dtype=torch.float32, device=dev)
         prev = torch.zeros_like(acc)
         for k0, cnt in chunks(k_lo, k_hi, group):
-            rec_flat = None
             img = plan.waverec(z, n * c, alphas=alphas[k0:k0 + cnt])
             if y is None:
                 g = input_gradient(self.model, img.view((cnt * n, c) + plan.rec_shape).unsqueeze(0), None, 1, 1,
@@ -273,10 +273,8 @@ class WaveletAttribution3D(BaseWAM3D):
             if shard.world == 1:
                 self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 2, prev=prev, k0=k0)
             else:
-                wk = np.array([0.0 if self.n_samples == 1 else (0.5 if k in (0, self.n_samples - 1) else 1.0)
-                               for k in range(k0, k0 + cnt)], dtype=np.float32)
-                self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 1, weights=torch.from_numpy(wk).to(dev))
-            del rec_flat
+                wk = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
+                self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 1, weights=wk)
         shard.all_reduce_sum(acc)
         out = (base.view(n, S, S, S) * acc.view(n, S, S, S)).cpu().numpy()
         self.grads = out
