@@ -41,6 +41,41 @@ def _to_numpy_2d(plan, flat, batch_items, n, c, first_item=0):
     return res
 
 
+def to_numpy(coeffs, dimension, grads=True):
+    """lib/wam_2D.py:10-48: coefficient containers (tensors with .grad) -> numpy containers."""
+    f = (lambda t: t.grad.detach().cpu().numpy()) if grads else (lambda t: t.detach().cpu().numpy())
+    if dimension == 1:
+        return [f(c) for c in coeffs]
+    if dimension == 2:
+        return [f(coeffs[0])] + [WaveletDetailTuple2d(f(c.horizontal), f(c.vertical), f(c.diagonal))
+                                 for c in coeffs[1:]]
+    raise ValueError("dimension must be 1 or 2")
+
+
+def _reproject_wam(coeffs, normalize_coeffs):
+    """lib/wam_2D.py:268-341 on host numpy coefficients (224 canvas, 224-based indices); the
+    reference's debugging prints (:334-335) are not reproduced."""
+    batch = coeffs[0].shape[0]
+    vis = np.zeros((batch, 224, 224))
+    ap = np.abs(coeffs[0].mean(axis=1))
+    if normalize_coeffs:
+        ap /= ap.max()
+    vis[:, :ap.shape[1], :ap.shape[2]] = ap
+    for i, coeff in enumerate(coeffs[1:][::-1]):
+        e, s = int(224 / 2 ** i), int(224 / 2 ** (i + 1))
+        hz = np.abs(coeff.horizontal.mean(axis=1))
+        vt = np.abs(coeff.vertical.mean(axis=1))
+        dg = np.abs(coeff.diagonal.mean(axis=1))
+        if normalize_coeffs:
+            hz /= hz.max()
+            dg /= dg.max()
+            vt /= vt.max()
+        vis[:, s:e, s:e] = dg[:, :(e - s), :(e - s)]
+        vis[:, s:e, :s] = vt[:, :(e - s), :(e - s)]
+        vis[:, :s, s:e] = hz[:, :(e - s), :(e - s)]
+    return vis
+
+
 def _bilinear_np(a, size):
     t = torch.as_tensor(np.ascontiguousarray(a))[None, None]
     return F.interpolate(t, size=(size, size), mode="bilinear", align_corners=False)[0, 0].numpy()
