@@ -52,7 +52,7 @@ int wam_plan_create(wam_plan** plan, int ndim, const int64_t* shape, int levels,
                     const double* rec_lo, const double* rec_hi, int filt_len, int mode);
 /* flags: WAM_PLAN_GENERIC forces the per-axis kernels (used by tests to cross-check the fused
  * 2D kernels); 0 selects the fastest path. wam_plan_create == wam_plan_create_ex(..., 0). */
-enum wam_plan_flags { WAM_PLAN_GENERIC = 1 };
+enum wam_plan_flags { WAM_PLAN_GENERIC = 1, WAM_PLAN_NO_ROWS = 2 };
 int wam_plan_create_ex(wam_plan** plan, int ndim, const int64_t* shape, int levels,
                        const double* dec_lo, const double* dec_hi,
                        const double* rec_lo, const double* rec_hi, int filt_len, int mode, int flags);
@@ -90,6 +90,41 @@ int wam_waverec(const wam_plan* plan, int64_t batch, const float* coeffs, const 
  * filters. grad: [batch, rec_shape...]; coeff_grads: band-major. */
 int wam_waverec_adjoint(const wam_plan* plan, int64_t batch, const float* grad, float* coeff_grads,
                         void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Fused WAM passes (2D, rows <= 512 samples, filter length in {2,4,6,8,12,16,20})
+ * ---------------------------------------------------------------------------------------------- */
+enum wam_caps { WAM_CAP_NOISY_WAVEDEC = 1, WAM_CAP_ADJOINT_MAPS = 2 };
+/* which fused entry points below this plan supports (bit set of wam_caps) */
+int wam_plan_caps(const wam_plan* plan);
+
+/* SmoothGrad sample generation fused into the first analysis level (lib/wam_2D.py:390-406):
+ * coeffs of x_i + sigma_i * N(0,1) for n_samples x images x channels planes, with the same
+ * Philox stream as wam_noise_add (counter (sample_base + s, image, element / 4)), without
+ * materialising the noisy input. x: [images, channels, H, W]; coeffs band-major over the
+ * (sample, image, channel) planes. WAM_ERR_UNSUPPORTED unless WAM_CAP_NOISY_WAVEDEC. */
+int wam_wavedec_noisy(const wam_plan* plan, int64_t n_samples, int64_t images, int channels,
+                      const float* x, const float* sigma, uint64_t seed, int64_t sample_base,
+                      float* coeffs, void* workspace, void* stream);
+
+/* Backward pass of waverec fused with the WAM epilogue (lib/wam_2D.py:116 loss.backward() through
+ * ptwt.waverec2, then :227-256 channel mean, |.|, batch-global max): for every image
+ * (groups x group_items, channels planes each) the item-major |mean_c| maps (as
+ * wam_subband_maps) and band_max[group, band] (caller zero-fills). coeff_grads != NULL also
+ * receives the per-channel coefficient gradients (band-major), e.g. for side attributes.
+ * WAM_ERR_UNSUPPORTED unless WAM_CAP_ADJOINT_MAPS and channels in {1, 3}. */
+int wam_waverec_adjoint_maps(const wam_plan* plan, int64_t groups, int64_t group_items, int channels,
+                             const float* grad, float* maps, float* band_max, float* coeff_grads,
+                             void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Live per-launch timing (profiling aid used by bench.py). While enabled every kernel launch is
+ * bracketed by hipEventRecord on its stream and logged with its kernel name and ALGORITHMIC
+ * bytes; wam_timing_drain synchronises on the recorded events, copies up to max_records
+ * (names: 64 chars each) and clears the log. Returns the number of records copied.
+ * ---------------------------------------------------------------------------------------------- */
+int wam_timing_enable(int on);
+int wam_timing_drain(int max_records, char* names, float* ms, double* bytes);
 
 /* ------------------------------------------------------------------------------------------------
  * SmoothGrad noise (lib/wam_2D.py:390-403, lib/wam_1D.py:311-322, lib/wam_3D.py:565-579)

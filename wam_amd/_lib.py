@@ -53,6 +53,11 @@ _SIGS = {
     "wam_accumulate_f32": (c_int, [c_i64, c_i64, c_vp, c_f32, c_vp, c_vp]),
     "wam_trapz_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "wam_reproject_scales": (c_int, [c_i64, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
+    "wam_plan_caps": (c_int, [c_vp]),
+    "wam_wavedec_noisy": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, ctypes.c_uint64, c_i64, c_vp, c_vp, c_vp]),
+    "wam_waverec_adjoint_maps": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "wam_timing_enable": (c_int, [c_int]),
+    "wam_timing_drain": (c_int, [c_int, ctypes.c_char_p, ctypes.POINTER(c_f32), ctypes.POINTER(ctypes.c_double)]),
 }
 
 for _name, (_res, _args) in _SIGS.items():

@@ -246,6 +246,7 @@ int launch_ana_L(int64_t batch, const float* in, int nh, int nw, int mh, int mw,
   nchunks = (mh + R - 1) / R;
   int64_t waves = base * nchunks;
   int64_t blocks = (waves + 3) / 4;
+  WamTimer tm(st, "k_dwt2_ana", 4.0 * (double)batch * ((double)nh * nw + 4.0 * mh * mw));
   hipLaunchKernelGGL(k_dwt2_ana<L>, dim3((unsigned)blocks), dim3(256), 0, st, in, nh, nw, (int64_t)nh * nw, oa, oh, ov,
                      od, mh, mw, (int64_t)mh * mw, p, mode, filt, nstrips, nchunks, R, waves);
   WAM_LAUNCH_CHECK();
@@ -268,6 +269,7 @@ int launch_syn_L(int64_t batch, const float* A, const float* H, const float* V, 
   nchunks = (nq + RQ - 1) / RQ;
   int64_t waves = base * nchunks;
   int64_t blocks = (waves + 3) / 4;
+  WamTimer tm(st, "k_dwt2_syn", 4.0 * (double)batch * (4.0 * mh * mw + (double)nh * nw));
   hipLaunchKernelGGL(k_dwt2_syn<L>, dim3((unsigned)blocks), dim3(256), 0, st, A, H, V, D, mh, mw, sa, sd, out, nh, nw,
                      p, filt, nstrips, nchunks, RQ, waves);
   WAM_LAUNCH_CHECK();

@@ -1,0 +1,557 @@
+// Row-resident fused 2D analysis kernels for gfx950 (rows up to 512 samples wide -- every 2D
+// config of the WAM path: 224^2 ImageNet crops and their pyramids, 512^2 for IG).
+//
+// One wave = one plane (or, for the adjoint epilogue, one image = C planes) x one strip of
+// 64*CPL output columns x one chunk of R output rows. The wave walks the extended input rows top
+// to bottom. Each source row is fetched WHOLE with 16-byte loads (one float4 per lane for 256
+// samples) one row ahead of its use, optionally gets its SmoothGrad noise added on the fly
+// (Philox4x32-10, 4 normals per lane per float4, the same stream as wam_noise_add), and is
+// committed to a wave-private LDS row. Boundary extension (reflect / symmetric / zero / replicate
+// / periodic) is pure index math on LDS reads, so no halo is staged and no noisy copy of the input
+// is ever written. Each lane filters its columns horizontally (ds_read_b64 pairs for interior
+// columns), pushes lo/hi into a register ring of the last L rows and, every second row, filters
+// the ring vertically into LL / H / V / D.
+//
+// k_adj_maps is the backward pass fused with the WAM epilogue (lib/wam_2D.py:227-256): zero-mode
+// analysis with reverse(rec) filters of all C channels of an image in one wave, then per
+// coefficient the numpy channel mean ((g0 + g1) + g2) / C, |.|, a wave-level running max per band
+// (one atomic max per wave and band: batch-global maxima per noise sample) and the item-major
+// |mean| maps the mosaic kernels gather from. LL stays per channel for the next level; the
+// per-channel detail gradients are only written when the caller asks for them (side attribute).
+#include "kernels.hpp"
+#include "rng.hpp"
+
+namespace {
+
+constexpr int kMaxRow = 512;
+constexpr int kWaves = 4;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float nan_max(float a, float b) { return (a != a || a > b) ? a : b; }
+
+// One source row held in registers: VEC-wide loads, MAXV per lane (VEC * 64 * MAXV >= kMaxRow).
+template <int VEC>
+struct RowRegs {
+  static constexpr int MAXV = kMaxRow / (64 * VEC);
+  float v[VEC * MAXV];
+
+  __device__ __forceinline__ void fetch(const float* __restrict__ row, int nw, int lane, bool valid) {
+#pragma unroll
+    for (int q = 0; q < MAXV; ++q) {
+      const int idx = (lane + 64 * q) * VEC;
+      if (valid && idx < nw) {
+        if constexpr (VEC == 4) {
+          float4 t = *reinterpret_cast<const float4*>(row + idx);
+          v[4 * q] = t.x;
+          v[4 * q + 1] = t.y;
+          v[4 * q + 2] = t.z;
+          v[4 * q + 3] = t.w;
+        } else {
+          v[q] = row[idx];
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < VEC; ++u) v[VEC * q + u] = 0.f;
+      }
+    }
+  }
+
+  // SmoothGrad noise for source row `sr` of channel c of image `img`, noise sample `smp`
+  // (element e = (c * nh + sr) * nw + idx of the image; group g = e / 4). Generated into `nz` at
+  // fetch time (independent of the loads, so they stay in flight) and added at commit time.
+  __device__ __forceinline__ void make_noise(float* nz, int nw, int lane, int64_t row_elem0, float sg, int64_t img,
+                                             int64_t smp, uint32_t k0, uint32_t k1) const {
+    static_assert(VEC == 4, "fused noise needs 16-byte rows");
+#pragma unroll
+    for (int q = 0; q < MAXV; ++q) {
+      const int idx = (lane + 64 * q) * 4;
+      float z[4] = {0.f, 0.f, 0.f, 0.f};
+      if (idx < nw) wam_normal4((row_elem0 + idx) >> 2, img, smp, k0, k1, z);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) nz[4 * q + u] = sg * z[u];
+    }
+  }
+
+  __device__ __forceinline__ void commit(float* lds, int nw, int lane, const float* nz = nullptr) const {
+#pragma unroll
+    for (int q = 0; q < MAXV; ++q) {
+      const int idx = (lane + 64 * q) * VEC;
+      if (idx < nw) {
+        if constexpr (VEC == 4) {
+          float4 o = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+          if (nz) {
+            o.x = o.x + nz[4 * q];
+            o.y = o.y + nz[4 * q + 1];
+            o.z = o.z + nz[4 * q + 2];
+            o.w = o.w + nz[4 * q + 3];
+          }
+          *reinterpret_cast<float4*>(lds + idx) = o;
+        } else {
+          lds[idx] = v[q];
+        }
+      }
+    }
+  }
+};
+
+// Horizontal analysis of output column j from the LDS row (ext column 2j - p + k).
+template <int L>
+__device__ __forceinline__ void hfilter(const float* lds, int j, int nw, int p, int mode, const float (&flo)[L],
+                                        const float (&fhi)[L], float& lo, float& hi) {
+  const int e0 = 2 * j - p;
+  float a = 0.f, d = 0.f;
+  if (e0 >= 0 && e0 + L <= nw) {
+    const float2* s2 = reinterpret_cast<const float2*>(lds + e0);  // e0 even (p = L - 2 is even)
+#pragma unroll
+    for (int k = 0; k < L; k += 2) {
+      float2 v = s2[k >> 1];
+      a = fmaf(flo[k], v.x, a);
+      d = fmaf(fhi[k], v.x, d);
+      a = fmaf(flo[k + 1], v.y, a);
+      d = fmaf(fhi[k + 1], v.y, d);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      const int s = wam_ext_index(e0 + k, nw, mode);
+      const float v = s >= 0 ? lds[s] : 0.f;
+      a = fmaf(flo[k], v, a);
+      d = fmaf(fhi[k], v, d);
+    }
+  }
+  lo = a;
+  hi = d;
+}
+
+// ------------------------------------------------------------------------------------------------
+template <int L, int CPL, int VEC, bool NOISE>
+__global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, int nh, int nw, int64_t in_plane,
+                                                  float* __restrict__ oa, float* __restrict__ oh,
+                                                  float* __restrict__ ov, float* __restrict__ od, int mh, int mw,
+                                                  int64_t out_plane, int p, int mode,
+                                                  const float* __restrict__ filt, int nstrips, int nchunks, int R,
+                                                  int64_t total_waves, WamNoise nz) {
+  __shared__ __attribute__((aligned(16))) float rows[kWaves][kMaxRow];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t gw = (int64_t)blockIdx.x * kWaves + wv;
+  if (gw >= total_waves) return;
+  const int chunk = (int)(gw % nchunks);
+  const int64_t t = gw / nchunks;
+  const int strip = (int)(t % nstrips);
+  const int64_t plane = t / nstrips;
+
+  float flo[L], fhi[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    flo[k] = filt[k];
+    fhi[k] = filt[L + k];
+  }
+  // NOISE: planes are (sample, image, channel); the clean input x holds (image, channel)
+  int64_t src_plane = plane, img = 0, smp = 0, ch = 0;
+  float sg = 0.f;
+  if constexpr (NOISE) {
+    const int64_t per_sample = nz.images * nz.channels;
+    src_plane = plane % per_sample;
+    smp = nz.sample_base + plane / per_sample;
+    img = src_plane / nz.channels;
+    ch = src_plane % nz.channels;
+    sg = nz.sigma[img];
+  }
+  const float* src = in + src_plane * in_plane;
+  float* lds = rows[wv];
+  const int j0 = strip * 64 * CPL;
+  const int i0 = chunk * R;
+  const int i1 = min(mh, i0 + R);
+  const int er0 = 2 * i0 - p;
+
+  RowRegs<VEC> f[2];
+  constexpr int NZ = NOISE ? RowRegs<VEC>::MAXV * VEC : 1;
+  float nzv[2][NZ];
+  auto fetch = [&](RowRegs<VEC>& r, float (&nzr)[NZ], int er) {
+    const int sr = wam_ext_index(er, nh, mode);
+    r.fetch(src + (int64_t)(sr < 0 ? 0 : sr) * nw, nw, lane, sr >= 0);
+    if constexpr (NOISE) {
+      // an out-of-range (zero) row of 'zero' mode carries no noise: the reference pads noisy_x
+      if (sr >= 0) r.make_noise(nzr, nw, lane, (ch * nh + sr) * (int64_t)nw, sg, img, smp, nz.k0, nz.k1);
+      else
+        for (int u = 0; u < NZ; ++u) nzr[u] = 0.f;
+    }
+  };
+  auto process = [&](const RowRegs<VEC>& r, const float (&nzr)[NZ], float (&lo)[CPL], float (&hi)[CPL]) {
+    r.commit(lds, nw, lane, NOISE ? nzr : nullptr);
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int j = j0 + lane + 64 * c;
+      if (j < mw) hfilter<L>(lds, j, nw, p, mode, flo, fhi, lo[c], hi[c]);
+      else lo[c] = hi[c] = 0.f;
+    }
+    wave_sync();
+  };
+
+  float rl[CPL][L], rh[CPL][L];
+  fetch(f[0], nzv[0], er0);
+#pragma unroll
+  for (int k = 0; k < L - 2; ++k) {
+    fetch(f[(k + 1) & 1], nzv[(k + 1) & 1], er0 + k + 1);
+    float lo[CPL], hi[CPL];
+    process(f[k & 1], nzv[k & 1], lo, hi);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      rl[c][k] = lo[c];
+      rh[c][k] = hi[c];
+    }
+  }
+  // invariant: f[0] holds ext row er0 + 2*(i - i0) + L - 2
+  for (int i = i0; i < i1; ++i) {
+    const int er = er0 + 2 * (i - i0) + L - 2;
+    fetch(f[1], nzv[1], er + 1);
+    float lo[CPL], hi[CPL];
+    process(f[0], nzv[0], lo, hi);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      rl[c][L - 2] = lo[c];
+      rh[c][L - 2] = hi[c];
+    }
+    if (i + 1 < i1) fetch(f[0], nzv[0], er + 2);
+    process(f[1], nzv[1], lo, hi);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      rl[c][L - 1] = lo[c];
+      rh[c][L - 1] = hi[c];
+    }
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int j = j0 + lane + 64 * c;
+      float a = 0.f, h = 0.f, v = 0.f, d = 0.f;
+#pragma unroll
+      for (int k = 0; k < L; ++k) {
+        a = fmaf(flo[k], rl[c][k], a);
+        h = fmaf(fhi[k], rl[c][k], h);
+        v = fmaf(flo[k], rh[c][k], v);
+        d = fmaf(fhi[k], rh[c][k], d);
+      }
+      if (j < mw) {
+        const int64_t o = plane * out_plane + (int64_t)i * mw + j;
+        oa[o] = a;
+        oh[o] = h;
+        ov[o] = v;
+        od[o] = d;
+      }
+#pragma unroll
+      for (int k = 0; k < L - 2; ++k) {
+        rl[c][k] = rl[c][k + 2];
+        rh[c][k] = rh[c][k + 2];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+struct MapsArgs {
+  float* maps;          // item-major packed |mean_c| maps, item = image
+  float* band_max;      // [groups, nbands]
+  float* full;          // optional band-major per-channel grads (planes = full_items)
+  int64_t maps_item;    // packed coefficients per item (plan coeff_numel)
+  int64_t off_h, off_v, off_d, off_a;  // per-item offsets of this level's bands (off_a < 0: not last)
+  int bh, bv, bd, ba;   // band indices
+  int nbands;
+  int64_t group_items;
+  int64_t full_items;
+};
+
+template <int L, int C, int VEC>
+__global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, int nh, int nw, int64_t in_plane,
+                                                  float* __restrict__ ll_out, int mh, int mw,
+                                                  const float* __restrict__ filt, int nstrips, int nchunks, int R,
+                                                  int64_t total_waves, MapsArgs ma) {
+  __shared__ __attribute__((aligned(16))) float rows[kWaves][C][kMaxRow];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t gw = (int64_t)blockIdx.x * kWaves + wv;
+  if (gw >= total_waves) return;
+  const int chunk = (int)(gw % nchunks);
+  const int64_t t = gw / nchunks;
+  const int strip = (int)(t % nstrips);
+  const int64_t img = t / nstrips;
+  constexpr int p = L - 2;
+
+  float flo[L], fhi[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    flo[k] = filt[k];
+    fhi[k] = filt[L + k];
+  }
+  const float* src = in + img * C * in_plane;
+  const int j = strip * 64 + lane;
+  const bool jv = j < mw;
+  const int i0 = chunk * R;
+  const int i1 = min(mh, i0 + R);
+  const int er0 = 2 * i0 - p;
+  const int64_t out_plane = (int64_t)mh * mw;
+
+  RowRegs<VEC> f[2][C];
+  auto fetch = [&](RowRegs<VEC> (&r)[C], int er) {
+    const bool valid = er >= 0 && er < nh;  // zero padding
+#pragma unroll
+    for (int c = 0; c < C; ++c) r[c].fetch(src + c * in_plane + (int64_t)(valid ? er : 0) * nw, nw, lane, valid);
+  };
+  auto process = [&](const RowRegs<VEC> (&r)[C], float (&lo)[C], float (&hi)[C]) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) r[c].commit(rows[wv][c], nw, lane);
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      if (jv) hfilter<L>(rows[wv][c], j, nw, p, WAM_MODE_ZERO, flo, fhi, lo[c], hi[c]);
+      else lo[c] = hi[c] = 0.f;
+    }
+    wave_sync();
+  };
+
+  float rl[C][L], rh[C][L];
+  fetch(f[0], er0);
+#pragma unroll
+  for (int k = 0; k < L - 2; ++k) {
+    fetch(f[(k + 1) & 1], er0 + k + 1);
+    float lo[C], hi[C];
+    process(f[k & 1], lo, hi);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      rl[c][k] = lo[c];
+      rh[c][k] = hi[c];
+    }
+  }
+  float mx_h = 0.f, mx_v = 0.f, mx_d = 0.f, mx_a = 0.f;
+  const bool last = ma.off_a >= 0;
+  float* mrow = ma.maps + img * ma.maps_item;
+  for (int i = i0; i < i1; ++i) {
+    const int er = er0 + 2 * (i - i0) + L - 2;
+    fetch(f[1], er + 1);
+    float lo[C], hi[C];
+    process(f[0], lo, hi);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      rl[c][L - 2] = lo[c];
+      rh[c][L - 2] = hi[c];
+    }
+    if (i + 1 < i1) fetch(f[0], er + 2);
+    process(f[1], lo, hi);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      rl[c][L - 1] = lo[c];
+      rh[c][L - 1] = hi[c];
+    }
+    float sa = 0.f, sh = 0.f, sv = 0.f, sd = 0.f;
+    const int64_t o = (int64_t)i * mw + j;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      float a = 0.f, h = 0.f, v = 0.f, d = 0.f;
+#pragma unroll
+      for (int k = 0; k < L; ++k) {
+        a = fmaf(flo[k], rl[c][k], a);
+        h = fmaf(fhi[k], rl[c][k], h);
+        v = fmaf(flo[k], rh[c][k], v);
+        d = fmaf(fhi[k], rh[c][k], d);
+      }
+      if (jv) {
+        const int64_t plane = img * C + c;
+        if (!last) ll_out[plane * out_plane + o] = a;
+        if (ma.full) {  // band-major: band b starts at full_items * off_b
+          ma.full[ma.full_items * ma.off_h + plane * out_plane + o] = h;
+          ma.full[ma.full_items * ma.off_v + plane * out_plane + o] = v;
+          ma.full[ma.full_items * ma.off_d + plane * out_plane + o] = d;
+          if (last) ma.full[ma.full_items * ma.off_a + plane * out_plane + o] = a;
+        }
+      }
+      // numpy float32 mean over the channel axis: sequential sum, then true_divide
+      if (c == 0) {
+        sa = a;
+        sh = h;
+        sv = v;
+        sd = d;
+      } else {
+        sa = sa + a;
+        sh = sh + h;
+        sv = sv + v;
+        sd = sd + d;
+      }
+#pragma unroll
+      for (int k = 0; k < L - 2; ++k) {
+        rl[c][k] = rl[c][k + 2];
+        rh[c][k] = rh[c][k + 2];
+      }
+    }
+    if (jv) {
+      const float mh_ = fabsf(sh / (float)C), mv_ = fabsf(sv / (float)C), md_ = fabsf(sd / (float)C);
+      mrow[ma.off_h + o] = mh_;
+      mrow[ma.off_v + o] = mv_;
+      mrow[ma.off_d + o] = md_;
+      mx_h = nan_max(mx_h, mh_);
+      mx_v = nan_max(mx_v, mv_);
+      mx_d = nan_max(mx_d, md_);
+      if (last) {
+        const float ma_ = fabsf(sa / (float)C);
+        mrow[ma.off_a + o] = ma_;
+        mx_a = nan_max(mx_a, ma_);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    mx_h = nan_max(mx_h, __shfl_xor(mx_h, s, 64));
+    mx_v = nan_max(mx_v, __shfl_xor(mx_v, s, 64));
+    mx_d = nan_max(mx_d, __shfl_xor(mx_d, s, 64));
+    mx_a = nan_max(mx_a, __shfl_xor(mx_a, s, 64));
+  }
+  if (lane == 0) {
+    unsigned int* bm = reinterpret_cast<unsigned int*>(ma.band_max + (img / ma.group_items) * ma.nbands);
+    atomicMax(bm + ma.bh, __float_as_uint(mx_h));
+    atomicMax(bm + ma.bv, __float_as_uint(mx_v));
+    atomicMax(bm + ma.bd, __float_as_uint(mx_d));
+    if (last) atomicMax(bm + ma.ba, __float_as_uint(mx_a));
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+constexpr int64_t kTargetWaves = 4096;
+
+void pick_chunks(int64_t base, int mh, int& nchunks, int& R) {
+  int64_t want = (kTargetWaves + base - 1) / base;
+  int maxchunks = (mh + 15) / 16;  // keep >= 16 output rows per chunk (halo L-2 rows per chunk)
+  if (maxchunks < 1) maxchunks = 1;
+  nchunks = (int)(want < 1 ? 1 : (want > maxchunks ? maxchunks : want));
+  R = (mh + nchunks - 1) / nchunks;
+  nchunks = (mh + R - 1) / R;
+}
+
+template <int L, int CPL, int VEC, bool NOISE>
+int launch_ana_rows_t(int64_t batch, const float* in, int nh, int nw, int mh, int mw, int mode, const float* filt,
+                      float* oa, float* oh, float* ov, float* od, const WamNoise* nz, hipStream_t st) {
+  const int nstrips = (mw + 64 * CPL - 1) / (64 * CPL);
+  int nchunks, R;
+  pick_chunks(batch * nstrips, mh, nchunks, R);
+  const int64_t waves = batch * nstrips * nchunks;
+  WamNoise z = nz ? *nz : WamNoise{nullptr, 1, 1, 0, 0, 0};
+  double bytes = 4.0 * ((double)batch * 4.0 * mh * mw + (nz ? (double)z.images * z.channels : (double)batch) * nh * nw);
+  WamTimer tm(st, NOISE ? "k_ana_rows<noise>" : "k_ana_rows", bytes);
+  hipLaunchKernelGGL((k_ana_rows<L, CPL, VEC, NOISE>), dim3((unsigned)((waves + kWaves - 1) / kWaves)), dim3(256), 0,
+                     st, in, nh, nw, (int64_t)nh * nw, oa, oh, ov, od, mh, mw, (int64_t)mh * mw, L - 2, mode, filt,
+                     nstrips, nchunks, R, waves, z);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+template <int L>
+int dispatch_ana(int64_t batch, const float* in, int nh, int nw, int mh, int mw, int mode, const float* filt,
+                 float* oa, float* oh, float* ov, float* od, const WamNoise* nz, hipStream_t st) {
+  const bool vec4 = (nw % 4 == 0) && ((uintptr_t)in % 16 == 0);
+  const bool cpl2 = mw > 64;
+  if (nz) {
+    if (!vec4) return WAM_ERR_UNSUPPORTED;
+    return cpl2 ? launch_ana_rows_t<L, 2, 4, true>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st)
+                : launch_ana_rows_t<L, 1, 4, true>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
+  }
+  if (vec4)
+    return cpl2 ? launch_ana_rows_t<L, 2, 4, false>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nullptr, st)
+                : launch_ana_rows_t<L, 1, 4, false>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nullptr, st);
+  return cpl2 ? launch_ana_rows_t<L, 2, 1, false>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nullptr, st)
+              : launch_ana_rows_t<L, 1, 1, false>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nullptr, st);
+}
+
+template <int L, int C>
+int launch_adj_t(int64_t images, const float* in, int nh, int nw, int mh, int mw, const float* filt, float* ll_out,
+                 const MapsArgs& ma, hipStream_t st) {
+  const int nstrips = (mw + 63) / 64;
+  int nchunks, R;
+  pick_chunks(images * nstrips, mh, nchunks, R);
+  const int64_t waves = images * nstrips * nchunks;
+  const bool last = ma.off_a >= 0;
+  double bytes = 4.0 * (double)images * ((double)C * nh * nw + 4.0 * mh * mw + (last ? 0.0 : (double)C * mh * mw) +
+                                         (ma.full ? (double)C * 4 * mh * mw : 0.0));
+  WamTimer tm(st, "k_adj_maps", bytes);
+  const bool vec4 = (nw % 4 == 0) && ((uintptr_t)in % 16 == 0);
+  if (vec4)
+    hipLaunchKernelGGL((k_adj_maps<L, C, 4>), dim3((unsigned)((waves + kWaves - 1) / kWaves)), dim3(256), 0, st, in,
+                       nh, nw, (int64_t)nh * nw, ll_out, mh, mw, filt, nstrips, nchunks, R, waves, ma);
+  else
+    hipLaunchKernelGGL((k_adj_maps<L, C, 1>), dim3((unsigned)((waves + kWaves - 1) / kWaves)), dim3(256), 0, st, in,
+                       nh, nw, (int64_t)nh * nw, ll_out, mh, mw, filt, nstrips, nchunks, R, waves, ma);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+template <int L>
+int dispatch_adj(int channels, int64_t images, const float* in, int nh, int nw, int mh, int mw, const float* filt,
+                 float* ll_out, const MapsArgs& ma, hipStream_t st) {
+  if (channels == 3) return launch_adj_t<L, 3>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+  if (channels == 1) return launch_adj_t<L, 1>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+  return WAM_ERR_UNSUPPORTED;
+}
+
+bool l_supported(int L) { return L == 2 || L == 4 || L == 6 || L == 8 || L == 12 || L == 16 || L == 20; }
+
+}  // namespace
+
+bool dwt2_rows_supported(const wam_plan* p, int level, bool adjoint) {
+  if (p->ndim != 2 || !l_supported(p->L)) return false;
+  const int64_t nw = (adjoint && level == 0) ? p->rec_shape[1] : p->lin[level][1];
+  return nw <= kMaxRow && nw >= 1;
+}
+
+int launch_dwt2_analysis_rows(const wam_plan* p, int64_t batch, const float* in, const int64_t* in_dims,
+                              const int64_t* out_dims, int mode, int fset, float* out_a, float* const* sub,
+                              const WamNoise* nz, hipStream_t st) {
+  const float* filt = p->d_filt + fset * p->L;
+  const int nh = (int)in_dims[0], nw = (int)in_dims[1], mh = (int)out_dims[0], mw = (int)out_dims[1];
+  float *oa = out_a, *oh = sub[0], *ov = sub[1], *od = sub[2];
+  switch (p->L) {
+    case 2: return dispatch_ana<2>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
+    case 4: return dispatch_ana<4>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
+    case 6: return dispatch_ana<6>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
+    case 8: return dispatch_ana<8>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
+    case 12: return dispatch_ana<12>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
+    case 16: return dispatch_ana<16>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
+    case 20: return dispatch_ana<20>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
+    default: return WAM_ERR_UNSUPPORTED;
+  }
+}
+
+int launch_dwt2_adjoint_maps_level(const wam_plan* p, int level, int64_t images, int channels, int64_t group_items,
+                                   const float* in, const int64_t* in_dims, float* ll_out, float* maps,
+                                   float* band_max, float* full_grads, int64_t full_items, hipStream_t st) {
+  const float* filt = p->d_filt + WAM_F_ADJ_LO * p->L;
+  const int nh = (int)in_dims[0], nw = (int)in_dims[1];
+  const int mh = (int)p->lout[level][0], mw = (int)p->lout[level][1];
+  MapsArgs ma;
+  ma.maps = maps;
+  ma.band_max = band_max;
+  ma.full = full_grads;
+  ma.maps_item = p->band_off[p->nbands];
+  ma.bh = wam_band_of(p, level, 0);
+  ma.bv = wam_band_of(p, level, 1);
+  ma.bd = wam_band_of(p, level, 2);
+  ma.ba = 0;
+  ma.off_h = p->band_off[ma.bh];
+  ma.off_v = p->band_off[ma.bv];
+  ma.off_d = p->band_off[ma.bd];
+  ma.off_a = (level == p->levels - 1) ? p->band_off[0] : -1;
+  ma.nbands = p->nbands;
+  ma.group_items = group_items;
+  ma.full_items = full_items;
+  switch (p->L) {
+    case 2: return dispatch_adj<2>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    case 4: return dispatch_adj<4>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    case 6: return dispatch_adj<6>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    case 8: return dispatch_adj<8>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    case 12: return dispatch_adj<12>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    case 16: return dispatch_adj<16>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    case 20: return dispatch_adj<20>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    default: return WAM_ERR_UNSUPPORTED;
+  }
+}

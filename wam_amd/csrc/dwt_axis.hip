@@ -70,6 +70,7 @@ int launch_analysis_axis(const float* in, float* lo, float* hi, int64_t outer, i
                          int mode, const float* flo, const float* fhi, int L, hipStream_t st) {
   int64_t work = outer * (int64_t)m * inner;
   if (work == 0) return WAM_OK;
+  WamTimer tm(st, "k_analysis_axis", 4.0 * (double)outer * inner * (n + 2.0 * m));
   hipLaunchKernelGGL(k_analysis_axis, dim3(wam_grid(work, 256)), dim3(256), 0, st, in, lo, hi, outer, n, m, inner,
                      padl, mode, flo, fhi, L);
   WAM_LAUNCH_CHECK();
@@ -80,6 +81,7 @@ int launch_synthesis_axis(const float* a, const float* d, float* out, int64_t ou
                           int p, const float* rlo, const float* rhi, int L, float sa, float sd, hipStream_t st) {
   int64_t work = outer * (int64_t)nout * inner;
   if (work == 0) return WAM_OK;
+  WamTimer tm(st, "k_synthesis_axis", 4.0 * (double)outer * inner * (2.0 * m + nout));
   hipLaunchKernelGGL(k_synthesis_axis, dim3(wam_grid(work, 256)), dim3(256), 0, st, a, d, out, outer, m, nout, inner,
                      p, rlo, rhi, L, sa, sd);
   WAM_LAUNCH_CHECK();

@@ -7,6 +7,7 @@
 #include <math.h>
 
 #include "kernels.hpp"
+#include "rng.hpp"
 
 namespace {
 
@@ -55,34 +56,9 @@ __global__ void __launch_bounds__(256) k_item_sigma(const float* __restrict__ x,
 }
 
 // ------------------------------------------------------------------------------ Philox noise
-struct u4 {
-  uint32_t x, y, z, w;
-};
-
-__device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
-  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
-    uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
-    c = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
-    k0 += W0;
-    k1 += W1;
-  }
-  return c;
-}
-
-__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
-  const float two32inv = 2.3283064365386963e-10f;  // 2^-32
-  float u1 = ((float)a + 1.0f) * two32inv;         // (0, 1]
-  float u2 = (float)b * two32inv;                  // [0, 1)
-  float r = sqrtf(-2.0f * logf(u1));
-  float s, c;
-  sincospif(2.0f * u2, &s, &c);
-  z0 = r * c;
-  z1 = r * s;
-}
-
+// One thread per group of 4 consecutive elements of an item: one Philox call -> 4 normals.
+// VEC4: item_stride % 4 == 0, so groups never straddle items and loads/stores are 16 B.
+template <bool VEC4>
 __global__ void __launch_bounds__(256) k_noise_add(int64_t n_samples, int64_t items, int64_t item_stride,
                                                    int64_t noised_len, const float* __restrict__ x,
                                                    const float* __restrict__ sigma,
@@ -96,16 +72,19 @@ __global__ void __launch_bounds__(256) k_noise_add(int64_t n_samples, int64_t it
     int64_t i = q % items;
     int64_t s = q / items;
     float z[4] = {0.f, 0.f, 0.f, 0.f};
-    if (!host_noise && 4 * g < noised_len) {
-      u4 c = {(uint32_t)g, (uint32_t)(g >> 32) ^ ((uint32_t)i << 8), (uint32_t)(sample_base + s), (uint32_t)i};
-      u4 r = philox4x32_10(c, k0, k1);
-      box_muller(r.x, r.y, z[0], z[1]);
-      box_muller(r.z, r.w, z[2], z[3]);
-    }
+    if (!host_noise && 4 * g < noised_len) wam_normal4(g, i, sample_base + s, k0, k1, z);
     const float sg = host_noise ? 0.f : sigma[i];
     const float* xi = x + i * item_stride;
     float* oi = out + (s * items + i) * item_stride;
     const float* hn = host_noise ? host_noise + (s * items + i) * item_stride : nullptr;
+    if (VEC4 && 4 * g + 4 <= noised_len) {
+      float4 xv = *reinterpret_cast<const float4*>(xi + 4 * g);
+      float4 nv;
+      if (hn) nv = *reinterpret_cast<const float4*>(hn + 4 * g);
+      else nv = make_float4(sg * z[0], sg * z[1], sg * z[2], sg * z[3]);
+      *reinterpret_cast<float4*>(oi + 4 * g) = make_float4(xv.x + nv.x, xv.y + nv.y, xv.z + nv.z, xv.w + nv.w);
+      continue;
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       int64_t e = 4 * g + u;
@@ -120,31 +99,36 @@ __global__ void __launch_bounds__(256) k_noise_add(int64_t n_samples, int64_t it
 
 // ------------------------------------------------------------------------------ subband maps
 struct BandTable {
-  int64_t off[WAM_MAX_BANDS + 1];  // per-item packed offsets
+  int64_t off[WAM_MAX_BANDS + 1];   // per-item packed offsets
+  int32_t tile0[WAM_MAX_BANDS + 1];  // first tile of each band (prefix over ceil(nb / TILE))
   int nbands;
 };
+constexpr int kMapTile = 1024;  // elements per block (4 per thread)
 
-// grid: x = chunk of the band, y = band, z = item. One atomic max per block and band.
+// grid: x = tile (over all bands), y = item. One atomic max per block.
 __global__ void __launch_bounds__(256) k_subband_maps(BandTable bt, int64_t items_total, int64_t group_items,
                                                       int channels, const float* __restrict__ g,
                                                       float* __restrict__ maps, float* __restrict__ band_max) {
-  const int b = blockIdx.y;
-  const int64_t item = blockIdx.z;
+  const int tile = blockIdx.x;
+  int b = 0;
+  while (b + 1 < bt.nbands && bt.tile0[b + 1] <= tile) ++b;
+  const int64_t item = blockIdx.y;
   const int64_t nb = bt.off[b + 1] - bt.off[b];
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if ((int64_t)blockIdx.x * blockDim.x >= nb) return;  // whole block idle
-  float v = 0.f;
-  const bool valid = q < nb;
-  if (valid) {
-    // band-major coefficient grads: band b holds [items_total * channels, nb]
-    const float* base = g + items_total * channels * bt.off[b] + (item * channels) * nb + q;
-    float acc = base[0];
-    for (int c = 1; c < channels; ++c) acc = acc + base[(int64_t)c * nb];
-    acc = acc / (float)channels;  // numpy mean: sum then true_divide
-    v = fabsf(acc);
-    maps[item * bt.off[bt.nbands] + bt.off[b] + q] = v;
+  const int64_t q0 = (int64_t)(tile - bt.tile0[b]) * kMapTile;
+  const float* base = g + items_total * channels * bt.off[b] + (item * channels) * nb;
+  float* out = maps + item * bt.off[bt.nbands] + bt.off[b];
+  float m = 0.f;
+#pragma unroll
+  for (int u = 0; u < kMapTile / 256; ++u) {
+    const int64_t q = q0 + u * 256 + threadIdx.x;
+    if (q < nb) {
+      float acc = base[q];
+      for (int c = 1; c < channels; ++c) acc = acc + base[(int64_t)c * nb + q];
+      float v = fabsf(acc / (float)channels);  // numpy mean: sum then true_divide
+      out[q] = v;
+      m = nan_max(m, v);
+    }
   }
-  float m = valid ? v : 0.f;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = nan_max(m, __shfl_xor(m, o, 64));
   __shared__ float sm[4];
@@ -367,9 +351,17 @@ int wam_noise_add(int64_t n_samples, int64_t items, int64_t item_stride, int64_t
   if (!host_noise && !sigma) return WAM_ERR_INVALID_ARG;
   int64_t work = n_samples * items * ((item_stride + 3) / 4);
   if (work == 0) return WAM_OK;
-  hipLaunchKernelGGL(k_noise_add, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, n_samples, items,
-                     item_stride, noised_len, x, sigma, host_noise, (uint32_t)seed, (uint32_t)(seed >> 32),
-                     sample_base, out);
+  WamTimer tm((hipStream_t)stream, item_stride % 4 == 0 ? "k_noise_add<v4>" : "k_noise_add",
+              4.0 * (double)items * item_stride * (1 + n_samples * (host_noise ? 2 : 1)));
+  if (item_stride % 4 == 0 && ((uintptr_t)x % 16 == 0) && ((uintptr_t)out % 16 == 0) &&
+      (!host_noise || (uintptr_t)host_noise % 16 == 0))
+    hipLaunchKernelGGL(k_noise_add<true>, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, n_samples,
+                       items, item_stride, noised_len, x, sigma, host_noise, (uint32_t)seed, (uint32_t)(seed >> 32),
+                       sample_base, out);
+  else
+    hipLaunchKernelGGL(k_noise_add<false>, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, n_samples,
+                       items, item_stride, noised_len, x, sigma, host_noise, (uint32_t)seed, (uint32_t)(seed >> 32),
+                       sample_base, out);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }
@@ -383,12 +375,15 @@ int wam_subband_maps(const wam_plan* p, int64_t groups, int64_t group_items, int
   if (items > 65535) return WAM_ERR_UNSUPPORTED;
   BandTable bt;
   bt.nbands = p->nbands;
-  int64_t maxb = 0;
-  for (int b = 0; b <= p->nbands; ++b) bt.off[b] = p->band_off[b];
-  for (int b = 0; b < p->nbands; ++b) maxb = std::max(maxb, p->band_off[b + 1] - p->band_off[b]);
-  dim3 grid((unsigned)((maxb + 255) / 256), (unsigned)p->nbands, (unsigned)items);
-  hipLaunchKernelGGL(k_subband_maps, grid, dim3(256), 0, (hipStream_t)stream, bt, items, group_items, channels,
-                     coeff_grads, maps, band_max);
+  int tiles = 0;
+  for (int b = 0; b <= p->nbands; ++b) {
+    bt.off[b] = p->band_off[b];
+    bt.tile0[b] = tiles;
+    if (b < p->nbands) tiles += (int)((p->band_off[b + 1] - p->band_off[b] + kMapTile - 1) / kMapTile);
+  }
+  WamTimer tm((hipStream_t)stream, "k_subband_maps", 4.0 * (double)items * (channels + 1) * p->band_off[p->nbands]);
+  hipLaunchKernelGGL(k_subband_maps, dim3((unsigned)tiles, (unsigned)items), dim3(256), 0, (hipStream_t)stream, bt,
+                     items, group_items, channels, coeff_grads, maps, band_max);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }
@@ -400,6 +395,8 @@ int wam_frame_accumulate(int64_t groups, int64_t group_items, int64_t frame_len,
   if (normalize && !band_max) return WAM_ERR_INVALID_ARG;
   int64_t work = group_items * frame_len;
   if (work == 0 || groups == 0) return WAM_OK;
+  WamTimer tm((hipStream_t)stream, "k_frame_accumulate",
+              4.0 * (double)groups * group_items * frame_len + 16.0 * group_items * frame_len + 8.0 * frame_len);
   hipLaunchKernelGGL(k_frame_accumulate, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, groups,
                      group_items, frame_len, src, band, maps, maps_item_len, band_max, n_bands, normalize, frame);
   WAM_LAUNCH_CHECK();
@@ -414,6 +411,8 @@ int wam_frame_trapz(int64_t groups, int64_t k0, int64_t group_items, int64_t fra
   if (normalize && !band_max) return WAM_ERR_INVALID_ARG;
   int64_t work = group_items * frame_len;
   if (work == 0 || groups == 0) return WAM_OK;
+  WamTimer tm((hipStream_t)stream, "k_frame_trapz",
+              4.0 * (double)groups * group_items * frame_len + 16.0 * group_items * frame_len + 8.0 * frame_len);
   hipLaunchKernelGGL(k_frame_trapz, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, groups, k0,
                      group_items, frame_len, src, band, maps, maps_item_len, band_max, n_bands, normalize, weights,
                      prev, acc);

@@ -16,3 +16,23 @@ int launch_dwt2_analysis_fused(const wam_plan* p, int64_t batch, const float* in
                                hipStream_t st);
 int launch_dwt2_synthesis_fused(const wam_plan* p, int64_t batch, int level, const float* a_in, float a_scale,
                                 const float* const* sub, float d_scale, float* out, hipStream_t st);
+
+#include "timing.hpp"
+
+// row-resident fused 2D kernels (dwt2_rows.hip): whole source rows staged in wave-private LDS
+bool dwt2_rows_supported(const wam_plan* p, int level, bool adjoint);
+int launch_dwt2_analysis_rows(const wam_plan* p, int64_t batch, const float* in, const int64_t* in_dims,
+                              const int64_t* out_dims, int mode, int fset, float* out_a, float* const* sub,
+                              const struct WamNoise* noise, hipStream_t st);
+int launch_dwt2_adjoint_maps_level(const wam_plan* p, int level, int64_t images, int channels, int64_t group_items,
+                                   const float* in, const int64_t* in_dims, float* ll_out, float* maps,
+                                   float* band_max, float* full_grads, int64_t full_items, hipStream_t st);
+
+// fused SmoothGrad noise on the analysis load (Philox4x32-10, same stream as wam_noise_add)
+struct WamNoise {
+  const float* sigma;     // per image
+  int64_t images;         // N (x holds N*C planes)
+  int channels;           // C
+  uint32_t k0, k1;        // seed
+  int64_t sample_base;
+};

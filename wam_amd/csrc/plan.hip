@@ -330,8 +330,18 @@ void band_ptrs(const wam_plan* p, int64_t batch, float* coeffs, int level, float
   for (int k = 0; k < per; ++k) sub[k] = coeffs + batch * p->band_off[wam_band_of(p, level, k)];
 }
 
+bool use_rows(const wam_plan* p, int level, bool adjoint) {
+  return p->ndim == 2 && !(p->flags & (WAM_PLAN_GENERIC | WAM_PLAN_NO_ROWS)) && dwt2_rows_supported(p, level, adjoint);
+}
+
+bool use_colstrip(const wam_plan* p) {
+  return p->ndim == 2 && !(p->flags & WAM_PLAN_GENERIC) && dwt2_fused_supported(p);
+}
+
+// noise (level 0 only): fused SmoothGrad noise on the load; `batch` then counts the virtual
+// (sample, image, channel) planes and x holds the clean (image, channel) planes.
 int analysis_driver(const wam_plan* p, int64_t batch, const float* x, float* coeffs, void* ws, hipStream_t st,
-                    bool adjoint) {
+                    bool adjoint, const WamNoise* noise = nullptr) {
   int nd = p->ndim;
   float* w = (float*)ws;
   int64_t ll = batch * wam_prod(p->lout[0], nd);
@@ -346,8 +356,13 @@ int analysis_driver(const wam_plan* p, int64_t batch, const float* x, float* coe
     float* sub[7];
     band_ptrs(p, batch, coeffs, l, sub);
     float* out_a = (l == p->levels - 1) ? coeffs : llbuf[l & 1];
+    const WamNoise* nz = (l == 0) ? noise : nullptr;
     int rc;
-    if (nd == 2 && !(p->flags & WAM_PLAN_GENERIC) && dwt2_fused_supported(p)) {
+    if (use_rows(p, l, adjoint)) {
+      rc = launch_dwt2_analysis_rows(p, batch, cur, in_dims, p->lout[l], mode, fset, out_a, sub, nz, st);
+    } else if (nz) {
+      rc = WAM_ERR_UNSUPPORTED;
+    } else if (use_colstrip(p)) {
       rc = launch_dwt2_analysis_fused(p, batch, cur, in_dims, p->lout[l], mode, fset, out_a, sub, st);
     } else {
       rc = generic_analysis_level(p, batch, cur, in_dims, p->lout[l], mode, fset, out_a, sub, tmp, st);
@@ -373,6 +388,51 @@ int wam_waverec_adjoint(const wam_plan* p, int64_t batch, const float* grad, flo
   if (!p || !grad || !coeff_grads || !ws || batch < 0) return WAM_ERR_INVALID_ARG;
   if (batch == 0) return WAM_OK;
   return analysis_driver(p, batch, grad, coeff_grads, ws, (hipStream_t)stream, true);
+}
+
+int wam_plan_caps(const wam_plan* p) {
+  if (!p) return 0;
+  int caps = 0;
+  bool rows_all = true;
+  for (int l = 0; l < p->levels; ++l) rows_all = rows_all && use_rows(p, l, true);
+  if (rows_all) caps |= WAM_CAP_ADJOINT_MAPS;
+  if (use_rows(p, 0, false) && p->lin[0][1] % 4 == 0) caps |= WAM_CAP_NOISY_WAVEDEC;
+  return caps;
+}
+
+int wam_wavedec_noisy(const wam_plan* p, int64_t n_samples, int64_t images, int channels, const float* x,
+                      const float* sigma, uint64_t seed, int64_t sample_base, float* coeffs, void* ws, void* stream) {
+  if (!p || !x || !sigma || !coeffs || !ws || n_samples < 0 || images < 0 || channels < 1) return WAM_ERR_INVALID_ARG;
+  if (!(wam_plan_caps(p) & WAM_CAP_NOISY_WAVEDEC)) return WAM_ERR_UNSUPPORTED;
+  const int64_t batch = n_samples * images * channels;
+  if (batch == 0) return WAM_OK;
+  WamNoise nz{sigma, images, channels, (uint32_t)seed, (uint32_t)(seed >> 32), sample_base};
+  return analysis_driver(p, batch, x, coeffs, ws, (hipStream_t)stream, false, &nz);
+}
+
+int wam_waverec_adjoint_maps(const wam_plan* p, int64_t groups, int64_t group_items, int channels, const float* grad,
+                             float* maps, float* band_max, float* coeff_grads, void* ws, void* stream) {
+  if (!p || !grad || !maps || !band_max || !ws || groups < 0 || group_items < 0 || channels < 1)
+    return WAM_ERR_INVALID_ARG;
+  if (!(wam_plan_caps(p) & WAM_CAP_ADJOINT_MAPS) || (channels != 1 && channels != 3)) return WAM_ERR_UNSUPPORTED;
+  const int64_t images = groups * group_items;
+  if (images == 0) return WAM_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t planes = images * channels;
+  float* w = (float*)ws;
+  int64_t ll = planes * wam_prod(p->lout[0], 2);
+  float* llbuf[2] = {w, w + ll};
+  const float* cur = grad;
+  for (int l = 0; l < p->levels; ++l) {
+    int64_t in_dims[2];
+    for (int a = 0; a < 2; ++a) in_dims[a] = (l == 0) ? p->rec_shape[a] : p->lin[l][a];
+    float* ll_out = (l == p->levels - 1) ? nullptr : llbuf[l & 1];
+    int rc = launch_dwt2_adjoint_maps_level(p, l, images, channels, group_items, cur, in_dims, ll_out, maps, band_max,
+                                            coeff_grads, planes, st);
+    if (rc) return rc;
+    cur = ll_out;
+  }
+  return WAM_OK;
 }
 
 int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha, int n_alpha, float* out,
@@ -412,6 +472,69 @@ int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const flo
     }
   }
   return WAM_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// Live per-launch timing (see timing.hpp)
+// ------------------------------------------------------------------------------------------------
+#include <atomic>
+#include <mutex>
+
+namespace {
+struct TimingRec {
+  const char* name;
+  hipEvent_t s, e;
+  double bytes;
+};
+std::atomic<int> g_timing{0};
+std::mutex g_timing_mu;
+std::vector<TimingRec> g_timing_recs;
+}  // namespace
+
+WamTimer::WamTimer(hipStream_t st_, const char* name_, double bytes_) : st(st_), name(name_), bytes(bytes_) {
+  if (!g_timing.load(std::memory_order_relaxed)) return;
+  if (hipEventCreate(&s) != hipSuccess || hipEventCreate(&e) != hipSuccess) {
+    s = e = nullptr;
+    return;
+  }
+  (void)hipEventRecord(s, st);
+}
+
+WamTimer::~WamTimer() {
+  if (!s) return;
+  (void)hipEventRecord(e, st);
+  std::lock_guard<std::mutex> lk(g_timing_mu);
+  g_timing_recs.push_back({name, s, e, bytes});
+}
+
+extern "C" {
+
+int wam_timing_enable(int on) {
+  g_timing.store(on ? 1 : 0);
+  return WAM_OK;
+}
+
+int wam_timing_drain(int max_records, char* names, float* ms, double* bytes) {
+  if (max_records < 0 || (max_records > 0 && (!names || !ms || !bytes))) return -WAM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(g_timing_mu);
+  int n = 0;
+  for (auto& r : g_timing_recs) {
+    if (n < max_records) {
+      float t = 0.f;
+      if (hipEventSynchronize(r.e) == hipSuccess) (void)hipEventElapsedTime(&t, r.s, r.e);
+      strncpy(names + 64 * n, r.name, 63);
+      names[64 * n + 63] = 0;
+      ms[n] = t;
+      bytes[n] = r.bytes;
+      ++n;
+    }
+    (void)hipEventDestroy(r.s);
+    (void)hipEventDestroy(r.e);
+  }
+  g_timing_recs.clear();
+  return n;
 }
 
 }  // extern "C"

@@ -1,0 +1,43 @@
+// Counter-based Philox4x32-10 + Box-Muller, shared by the standalone noise kernel and the fused
+// noisy analysis so both produce the same stream: counter = (g, (g >> 32) ^ (item << 8),
+// sample, item) with g = element index within the item / 4; key = seed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct wam_u4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ wam_u4 wam_philox4x32_10(wam_u4 c, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    c = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+__device__ __forceinline__ void wam_box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
+  const float two32inv = 2.3283064365386963e-10f;  // 2^-32
+  float u1 = ((float)a + 1.0f) * two32inv;         // (0, 1]
+  float u2 = (float)b * two32inv;                  // [0, 1)
+  float r = sqrtf(-2.0f * logf(u1));
+  float s, c;
+  sincospif(2.0f * u2, &s, &c);
+  z0 = r * c;
+  z1 = r * s;
+}
+
+// four N(0,1) values for element group g of `item` in `sample`
+__device__ __forceinline__ void wam_normal4(int64_t g, int64_t item, int64_t sample, uint32_t k0, uint32_t k1,
+                                            float z[4]) {
+  wam_u4 c = {(uint32_t)g, (uint32_t)(g >> 32) ^ ((uint32_t)item << 8), (uint32_t)sample, (uint32_t)item};
+  wam_u4 r = wam_philox4x32_10(c, k0, k1);
+  wam_box_muller(r.x, r.y, z[0], z[1]);
+  wam_box_muller(r.z, r.w, z[2], z[3]);
+}

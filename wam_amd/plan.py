@@ -153,19 +153,76 @@ class Plan:
             check(lib.wam_waverec_adjoint(self._h, batch, ptr(grad), ptr(out), ptr(ws), stream_of(grad.device)))
         return out
 
+    # ---------------------------------------------------------------- fused WAM passes
+    @property
+    def caps(self):
+        return lib.wam_plan_caps(self._h)
 
-def get_plan(ndim, shape, levels, wavelet, mode, device, generic=False):
+    def wavedec_noisy(self, x, sigma, n_samples, images, channels, seed, sample_base=0, out=None):
+        """coefficients of x + sigma_i N(0,1) (Philox) for n_samples x images x channels planes."""
+        require_cuda(x, "x")
+        x = x.contiguous()
+        batch = n_samples * images * channels
+        if out is None:
+            out = torch.empty(batch * self.coeff_numel, dtype=torch.float32, device=x.device)
+        ws = self.workspace(batch)
+        check(lib.wam_wavedec_noisy(self._h, n_samples, images, channels, ptr(x), ptr(sigma),
+                                    ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), sample_base, ptr(out), ptr(ws),
+                                    stream_of(x.device)))
+        return out
+
+    def adjoint_maps(self, grad, groups, group_items, channels, full=False):
+        """waverec VJP fused with the channel-mean |.| epilogue -> (maps, band_max[, coeff grads])."""
+        require_cuda(grad, "grad")
+        grad = grad.contiguous()
+        images = groups * group_items
+        dev = grad.device
+        maps = torch.empty(images * self.coeff_numel, dtype=torch.float32, device=dev)
+        bmax = torch.zeros((groups, self.nbands), dtype=torch.float32, device=dev)
+        cg = torch.empty(images * channels * self.coeff_numel, dtype=torch.float32, device=dev) if full else None
+        ws = self.workspace(images * channels)
+        check(lib.wam_waverec_adjoint_maps(self._h, groups, group_items, channels, ptr(grad), ptr(maps), ptr(bmax),
+                                           ptr(cg), ptr(ws), stream_of(dev)))
+        return maps, bmax, cg
+
+
+def get_plan(ndim, shape, levels, wavelet, mode, device, generic=False, flags=None):
     w = filters.get_wavelet(wavelet)
     device = torch.device(device)
     if device.index is None:
         device = torch.device("cuda", torch.cuda.current_device())
-    key = (ndim, tuple(int(s) for s in shape), int(levels), w, mode, device, bool(generic))
+    fl = (PLAN_GENERIC if generic else 0) if flags is None else int(flags)
+    key = (ndim, tuple(int(s) for s in shape), int(levels), w, mode, device, fl)
     with _LOCK:
         p = _CACHE.get(key)
         if p is None:
-            p = Plan(ndim, shape, levels, w, mode, device, PLAN_GENERIC if generic else 0)
+            p = Plan(ndim, shape, levels, w, mode, device, fl)
             _CACHE[key] = p
     return p
+
+
+PLAN_NO_ROWS = 2
+CAP_NOISY_WAVEDEC = 1
+CAP_ADJOINT_MAPS = 2
+
+
+def timing_enable(on=True):
+    lib.wam_timing_enable(1 if on else 0)
+
+
+def timing_drain():
+    """[(kernel name, ms, algorithmic bytes)] for every launch since the last drain."""
+    out = []
+    cap = 4096
+    while True:
+        names = ctypes.create_string_buffer(64 * cap)
+        ms = (c_f32 * cap)()
+        nb = (ctypes.c_double * cap)()
+        n = lib.wam_timing_drain(cap, names, ms, nb)
+        for i in range(n):
+            out.append((names.raw[64 * i:64 * (i + 1)].split(b"\0", 1)[0].decode(), ms[i], nb[i]))
+        if n < cap:
+            return out
 
 
 # -------------------------------------------------------------------- WAM epilogue wrappers

@@ -26,7 +26,8 @@ from . import frames
 from .constants import WaveletDetailTuple2d
 from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, legacy_noise, model_device,
                      require_gpu_device)
-from .plan import frame_accumulate, frame_trapz, get_plan, item_sigma, noise_add, reproject_scales, subband_maps
+from .plan import (CAP_ADJOINT_MAPS, CAP_NOISY_WAVEDEC, frame_accumulate, frame_trapz, get_plan, item_sigma,
+                   noise_add, reproject_scales, subband_maps)
 
 
 def _to_numpy_2d(plan, flat, batch_items, n, c, first_item=0):
@@ -159,6 +160,16 @@ class BaseWAM2D:
         self._scales = v
 
     # ------------------------------------------------------------------ reference API
+    @staticmethod
+    def _adjoint_maps(plan, g, groups, n, c, full):
+        """Backward of waverec2 + channel-mean |.| maps + per-sample band maxima: one fused HIP
+        pass when the plan supports it, else the adjoint followed by wam_subband_maps."""
+        if (plan.caps & CAP_ADJOINT_MAPS) and c in (1, 3):
+            return plan.adjoint_maps(g, groups, n, c, full=full)
+        cg = plan.adjoint(g)
+        maps, bmax = subband_maps(plan, cg, groups, n, c)
+        return maps, bmax, cg
+
     def _coeff_plan(self, coeffs):
         """Plan for an explicit coefficient list (image=False): the even spatial size whose
         decomposition has these coefficient shapes (what ptwt.waverec2 reconstructs)."""
@@ -187,9 +198,8 @@ class BaseWAM2D:
             flat = torch.cat([b.detach().to(dev, torch.float32).reshape(-1) for b in bands])
         img = plan.waverec(flat, n * c)[0].view((n, c) + plan.rec_shape)
         g = input_gradient(self.model, img, y, 1, n, self.autocast_dtype, self.channels_last)
-        cg = plan.adjoint(g.view((n * c,) + plan.rec_shape))
+        maps, bmax, cg = self._adjoint_maps(plan, g.view((n * c,) + plan.rec_shape), 1, n, c, full=True)
         self._record_pass(plan, flat, cg, n * c, 0, n, c)
-        maps, bmax = subband_maps(plan, cg, 1, n, c)
         if self.frame == "native":
             canvas, base = plan.shape, plan.shape
         else:
@@ -305,19 +315,25 @@ class WaveletAttribution2D(BaseWAM2D):
                                     list(range(s_lo, s_hi)))
         rec = plan.rec_shape
         last = None
-        for s0, cnt in chunks(s_lo, s_hi, group):
-            host = None
+        work = chunks(s_lo, s_hi, group)
+        for ci, (s0, cnt) in enumerate(work):
+            is_last = ci == len(work) - 1
             if noise_it is not None:
                 arr = np.stack([next(noise_it)[1] for _ in range(cnt)])
                 host = torch.from_numpy(arr).pin_memory().to(dev, non_blocking=True)
-            noisy = noise_add(x, sigma, cnt, n, item, item, seed=self.random_seed, sample_base=s0, host_noise=host)
-            flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
+                noisy = noise_add(x, sigma, cnt, n, item, item, host_noise=host)
+                flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
+            elif plan.caps & CAP_NOISY_WAVEDEC:
+                flat = plan.wavedec_noisy(x, sigma, cnt, n, c, self.random_seed, s0)  # noise fused on the load
+            else:
+                noisy = noise_add(x, sigma, cnt, n, item, item, seed=self.random_seed, sample_base=s0)
+                flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
             img = plan.waverec(flat, cnt * n * c)[0].view((cnt * n, c) + rec)
             g = input_gradient(self.model, img, y, cnt, n, self.autocast_dtype, self.channels_last)
-            cg = plan.adjoint(g.view((cnt * n * c,) + rec))
-            maps, bmax = subband_maps(plan, cg, cnt, n, c)
+            maps, bmax, cg = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=is_last)
             frame_accumulate(cnt, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, frame)
-            last = (plan, flat, cg, cnt * n * c, (cnt - 1) * n, n, c)
+            if is_last:
+                last = (plan, flat, cg, cnt * n * c, (cnt - 1) * n, n, c)
         if last is not None:
             self.wam._record_pass(*last)
         shard.all_reduce_sum(frame)
@@ -344,11 +360,12 @@ class WaveletAttribution2D(BaseWAM2D):
         prev = torch.zeros_like(acc)
         rec = plan.rec_shape
         last = None
-        for k0, cnt in chunks(k_lo, k_hi, group):
+        work = chunks(k_lo, k_hi, group)
+        for ci, (k0, cnt) in enumerate(work):
             img = plan.waverec(z, n * c, alphas=alphas[k0:k0 + cnt]).view((cnt * n, c) + rec)
             g = input_gradient(self.model, img, y, cnt, n, self.autocast_dtype, self.channels_last)
-            cg = plan.adjoint(g.view((cnt * n * c,) + rec))
-            maps, bmax = subband_maps(plan, cg, cnt, n, c)
+            maps, bmax, cg = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c,
+                                                full=ci == len(work) - 1)
             weights = None
             if shard.world > 1:
                 weights = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
