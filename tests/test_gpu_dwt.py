@@ -187,3 +187,54 @@ def test_matlab_known_answers(wam):
         _, got = _run_dec(wam, x, 1, 1, wav, mode, generic=True)
         assert max_rel(got[0][0], d[c + "_ma"]) < 1e-5, c
         assert max_rel(got[1][0], d[c + "_md"]) < 1e-5, c
+
+
+# ------------------------------------------------------------------------------ fused WAM passes
+@pytest.mark.parametrize("wav,shape,J,mode", [("db4", (224, 224), 3, "reflect"), ("haar", (224, 224), 3, "zero"),
+                                              ("sym8", (96, 128), 2, "symmetric"), ("db6", (60, 44), 2, "constant"),
+                                              ("haar", (512, 512), 5, "periodic")])
+def test_rows_colstrip_generic_agree(wam, wav, shape, J, mode):
+    """The three 2D analysis implementations (row-resident, column-strip, per-axis) agree."""
+    torch.manual_seed(5)
+    B = 6
+    x = torch.randn((B,) + shape, device="cuda")
+    rows = wam.get_plan(2, shape, J, wav, mode, "cuda")
+    col = wam.get_plan(2, shape, J, wav, mode, "cuda", flags=wam.PLAN_NO_ROWS)
+    gen = wam.get_plan(2, shape, J, wav, mode, "cuda", generic=True)
+    cr, cc, cg = rows.wavedec(x), col.wavedec(x), gen.wavedec(x)
+    assert torch.equal(cr, cc)
+    assert (cr - cg).abs().max().item() <= 1e-5 * cg.abs().max().item()
+    g = torch.randn((B,) + rows.rec_shape, device="cuda")
+    ar, ac, ag = rows.adjoint(g), col.adjoint(g), gen.adjoint(g)
+    assert torch.equal(ar, ac)
+    assert (ar - ag).abs().max().item() <= 1e-5 * ag.abs().max().item()
+
+
+@pytest.mark.parametrize("wav,J", [("db4", 3), ("haar", 3), ("sym8", 2)])
+def test_noisy_wavedec_equals_noise_then_wavedec(wam, wav, J):
+    p = wam.get_plan(2, (224, 224), J, wav, "reflect", "cuda")
+    assert p.caps & wam.CAP_NOISY_WAVEDEC
+    torch.manual_seed(6)
+    N, C, S = 5, 3, 3
+    x = torch.randn(N, C, 224, 224, device="cuda")
+    sigma = wam.item_sigma(x, C * 224 * 224, C * 224 * 224, 0.25)
+    fused = p.wavedec_noisy(x, sigma, S, N, C, seed=1234, sample_base=7)
+    noisy = wam.noise_add(x, sigma, S, N, C * 224 * 224, C * 224 * 224, seed=1234, sample_base=7)
+    ref = p.wavedec(noisy.view(S * N * C, 224, 224))
+    assert torch.equal(fused, ref)
+
+
+@pytest.mark.parametrize("wav,shape,J,C", [("db4", (224, 224), 3, 3), ("haar", (224, 224), 3, 3),
+                                           ("sym8", (128, 96), 2, 1), ("db6", (225, 223), 3, 3)])
+def test_adjoint_maps_equals_adjoint_then_subband_maps(wam, wav, shape, J, C):
+    p = wam.get_plan(2, shape, J, wav, "reflect", "cuda")
+    assert p.caps & wam.CAP_ADJOINT_MAPS
+    torch.manual_seed(7)
+    G, N = 3, 4
+    g = torch.randn((G * N * C,) + p.rec_shape, device="cuda")
+    maps, bmax, full = p.adjoint_maps(g, G, N, C, full=True)
+    cg = p.adjoint(g)
+    rmaps, rbmax = wam.subband_maps(p, cg, G, N, C)
+    assert torch.equal(full, cg)
+    assert torch.equal(maps, rmaps)
+    assert torch.equal(bmax, rbmax)

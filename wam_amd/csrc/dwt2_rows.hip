@@ -3,14 +3,16 @@
 //
 // One wave = one plane (or, for the adjoint epilogue, one image = C planes) x one strip of
 // 64*CPL output columns x one chunk of R output rows. The wave walks the extended input rows top
-// to bottom. Each source row is fetched WHOLE with 16-byte loads (one float4 per lane for 256
-// samples) one row ahead of its use, optionally gets its SmoothGrad noise added on the fly
-// (Philox4x32-10, 4 normals per lane per float4, the same stream as wam_noise_add), and is
-// committed to a wave-private LDS row. Boundary extension (reflect / symmetric / zero / replicate
-// / periodic) is pure index math on LDS reads, so no halo is staged and no noisy copy of the input
-// is ever written. Each lane filters its columns horizontally (ds_read_b64 pairs for interior
-// columns), pushes lo/hi into a register ring of the last L rows and, every second row, filters
-// the ring vertically into LL / H / V / D.
+// to bottom. Each source row is fetched WHOLE with 16-byte loads (one float4 per lane covers 256
+// samples) one row ahead of its use -- branch-free (clamped addresses + selects) so the compiler
+// can keep the next row in flight with a counted vmcnt -- optionally gets its SmoothGrad noise
+// generated at fetch time and added at commit time (Philox4x32-10, 4 normals per lane per float4,
+// the same stream as wam_noise_add), and is committed to a wave-private LDS row that carries the
+// boundary extension in explicit pad slots (refreshed per row from per-lane precomputed source
+// columns; zero padding is written once). No halo is staged from HBM and no noisy copy of the input
+// is ever written. Each lane filters its columns horizontally (ds_read_b64 pairs), pushes lo/hi
+// into a register ring of the last L rows and, every second row, filters the ring vertically
+// into LL / H / V / D.
 //
 // k_adj_maps is the backward pass fused with the WAM epilogue (lib/wam_2D.py:227-256): zero-mode
 // analysis with reverse(rec) filters of all C channels of an image in one wave, then per
@@ -18,125 +20,147 @@
 // (one atomic max per wave and band: batch-global maxima per noise sample) and the item-major
 // |mean| maps the mosaic kernels gather from. LL stays per channel for the next level; the
 // per-channel detail gradients are only written when the caller asks for them (side attribute).
+//
+// Waves are independent (no workgroup barriers). LDS writes and reads of a wave-private row are
+// ordered by the wave's in-order LDS queue; __builtin_amdgcn_wave_barrier() keeps the compiler
+// from reordering them.
 #include "kernels.hpp"
 #include "rng.hpp"
 
 namespace {
 
 constexpr int kMaxRow = 512;
+constexpr int kPadL = 24;              // >= p = L - 2 for L <= 20, multiple of 4 (16-byte commits)
+constexpr int kRowLds = kPadL + kMaxRow + 32;
 constexpr int kWaves = 4;
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+__device__ __forceinline__ void wsync() { __builtin_amdgcn_wave_barrier(); }
 
 __device__ __forceinline__ float nan_max(float a, float b) { return (a != a || a > b) ? a : b; }
 
-// One source row held in registers: VEC-wide loads, MAXV per lane (VEC * 64 * MAXV >= kMaxRow).
-template <int VEC>
-struct RowRegs {
-  static constexpr int MAXV = kMaxRow / (64 * VEC);
-  float v[VEC * MAXV];
+__device__ __attribute__((noinline)) int ext_slow(int i, int n, int mode) { return wam_ext_index(i, n, mode); }
 
+// source row of extended row er (-1 = zero row), fast path for the interior
+__device__ __forceinline__ int row_src(int er, int n, int mode) {
+  return (er >= 0 && er < n) ? er : ext_slow(er, n, mode);
+}
+
+// One source row in registers: VEC-wide loads, MAXV per lane.
+template <int VEC, int MAXV>
+struct RowRegs {
+  float v[VEC * MAXV];
+  bool ok[MAXV];
+
+  // branch-free: out-of-range lanes / rows load a clamped valid address; the zeroing select is
+  // deferred to commit() so the load stays in flight until the row is consumed
   __device__ __forceinline__ void fetch(const float* __restrict__ row, int nw, int lane, bool valid) {
 #pragma unroll
     for (int q = 0; q < MAXV; ++q) {
       const int idx = (lane + 64 * q) * VEC;
-      if (valid && idx < nw) {
-        if constexpr (VEC == 4) {
-          float4 t = *reinterpret_cast<const float4*>(row + idx);
-          v[4 * q] = t.x;
-          v[4 * q + 1] = t.y;
-          v[4 * q + 2] = t.z;
-          v[4 * q + 3] = t.w;
-        } else {
-          v[q] = row[idx];
-        }
+      ok[q] = valid && idx < nw;
+      const int ci = idx < nw ? idx : nw - VEC;
+      if constexpr (VEC == 4) {
+        float4 t = *reinterpret_cast<const float4*>(row + ci);
+        v[4 * q] = t.x;
+        v[4 * q + 1] = t.y;
+        v[4 * q + 2] = t.z;
+        v[4 * q + 3] = t.w;
       } else {
-#pragma unroll
-        for (int u = 0; u < VEC; ++u) v[VEC * q + u] = 0.f;
+        v[q] = row[ci];
       }
     }
   }
 
-  // SmoothGrad noise for source row `sr` of channel c of image `img`, noise sample `smp`
-  // (element e = (c * nh + sr) * nw + idx of the image; group g = e / 4). Generated into `nz` at
-  // fetch time (independent of the loads, so they stay in flight) and added at commit time.
-  __device__ __forceinline__ void make_noise(float* nz, int nw, int lane, int64_t row_elem0, float sg, int64_t img,
-                                             int64_t smp, uint32_t k0, uint32_t k1) const {
-    static_assert(VEC == 4, "fused noise needs 16-byte rows");
-#pragma unroll
-    for (int q = 0; q < MAXV; ++q) {
-      const int idx = (lane + 64 * q) * 4;
-      float z[4] = {0.f, 0.f, 0.f, 0.f};
-      if (idx < nw) wam_normal4((row_elem0 + idx) >> 2, img, smp, k0, k1, z);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) nz[4 * q + u] = sg * z[u];
-    }
-  }
-
-  __device__ __forceinline__ void commit(float* lds, int nw, int lane, const float* nz = nullptr) const {
+  // commit to the padded LDS row (sample s at lds[kPadL + s]); noise (optional) added here
+  __device__ __forceinline__ void commit(float* lds, int lane, const float* nz) const {
 #pragma unroll
     for (int q = 0; q < MAXV; ++q) {
       const int idx = (lane + 64 * q) * VEC;
-      if (idx < nw) {
-        if constexpr (VEC == 4) {
-          float4 o = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-          if (nz) {
-            o.x = o.x + nz[4 * q];
-            o.y = o.y + nz[4 * q + 1];
-            o.z = o.z + nz[4 * q + 2];
-            o.w = o.w + nz[4 * q + 3];
-          }
-          *reinterpret_cast<float4*>(lds + idx) = o;
-        } else {
-          lds[idx] = v[q];
+      if constexpr (VEC == 4) {
+        float4 o = ok[q] ? make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3])
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (nz) {
+          o.x += nz[4 * q];
+          o.y += nz[4 * q + 1];
+          o.z += nz[4 * q + 2];
+          o.w += nz[4 * q + 3];
         }
+        *reinterpret_cast<float4*>(lds + kPadL + idx) = o;
+      } else {
+        lds[kPadL + idx] = ok[q] ? v[q] : 0.f;
       }
     }
   }
 };
 
-// Horizontal analysis of output column j from the LDS row (ext column 2j - p + k).
+// SmoothGrad noise for one fetched row (group g = e / 4 with e = (c*nh + sr)*nw + idx)
+template <int MAXV>
+__device__ __forceinline__ void make_noise(float (&nz)[4 * MAXV], int nw, int lane, int64_t row_elem0, float sg,
+                                           int64_t img, int64_t smp, uint32_t k0, uint32_t k1, bool valid) {
+#pragma unroll
+  for (int q = 0; q < MAXV; ++q) {
+    const int idx = (lane + 64 * q) * 4;
+    float z[4];
+    wam_normal4((row_elem0 + (idx < nw ? idx : 0)) >> 2, img, smp, k0, k1, z);
+    const bool ok = valid && idx < nw;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) nz[4 * q + u] = ok ? sg * z[u] : 0.f;
+  }
+}
+
+// pad-slot refresh: lane t < npad owns ext column ext_col (left pads t - p, right pads nw + ...)
+struct PadLane {
+  int dst;   // lds index of the pad slot (or -1: this lane owns none)
+  int src;   // lds index of its source sample (or -1: zero)
+};
+
+__device__ __forceinline__ PadLane pad_lane(int lane, int nw, int p, int mode) {
+  const int npad_r = p + (nw & 1) + 1;  // right pads (one spare)
+  PadLane pl{-1, -1};
+  int e;
+  if (lane < p) e = lane - p;
+  else if (lane < p + npad_r) e = nw + (lane - p);
+  else return pl;
+  pl.dst = kPadL + e;
+  const int s = wam_ext_index(e, nw, mode);
+  pl.src = s >= 0 ? kPadL + s : -1;
+  return pl;
+}
+
+__device__ __forceinline__ void refresh_pads(float* lds, const PadLane& pl) {
+  float v = 0.f;
+  if (pl.src >= 0) v = lds[pl.src];
+  wsync();
+  if (pl.dst >= 0) lds[pl.dst] = v;
+}
+
+// Horizontal analysis of output column j from the padded LDS row (ext column 2j - p + k).
 template <int L>
-__device__ __forceinline__ void hfilter(const float* lds, int j, int nw, int p, int mode, const float (&flo)[L],
-                                        const float (&fhi)[L], float& lo, float& hi) {
-  const int e0 = 2 * j - p;
+__device__ __forceinline__ void hfilter(const float* lds, int j, int p, const float (&flo)[L], const float (&fhi)[L],
+                                        float& lo, float& hi) {
+  const float2* s2 = reinterpret_cast<const float2*>(lds + kPadL + 2 * j - p);  // even offset (p even)
   float a = 0.f, d = 0.f;
-  if (e0 >= 0 && e0 + L <= nw) {
-    const float2* s2 = reinterpret_cast<const float2*>(lds + e0);  // e0 even (p = L - 2 is even)
 #pragma unroll
-    for (int k = 0; k < L; k += 2) {
-      float2 v = s2[k >> 1];
-      a = fmaf(flo[k], v.x, a);
-      d = fmaf(fhi[k], v.x, d);
-      a = fmaf(flo[k + 1], v.y, a);
-      d = fmaf(fhi[k + 1], v.y, d);
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < L; ++k) {
-      const int s = wam_ext_index(e0 + k, nw, mode);
-      const float v = s >= 0 ? lds[s] : 0.f;
-      a = fmaf(flo[k], v, a);
-      d = fmaf(fhi[k], v, d);
-    }
+  for (int k = 0; k < L; k += 2) {
+    const float2 v = s2[k >> 1];
+    a = fmaf(flo[k], v.x, a);
+    d = fmaf(fhi[k], v.x, d);
+    a = fmaf(flo[k + 1], v.y, a);
+    d = fmaf(fhi[k + 1], v.y, d);
   }
   lo = a;
   hi = d;
 }
 
 // ------------------------------------------------------------------------------------------------
-template <int L, int CPL, int VEC, bool NOISE>
+template <int L, int CPL, int VEC, int MAXV, bool NOISE>
 __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, int nh, int nw, int64_t in_plane,
                                                   float* __restrict__ oa, float* __restrict__ oh,
                                                   float* __restrict__ ov, float* __restrict__ od, int mh, int mw,
-                                                  int64_t out_plane, int p, int mode,
-                                                  const float* __restrict__ filt, int nstrips, int nchunks, int R,
-                                                  int64_t total_waves, WamNoise nz) {
-  __shared__ __attribute__((aligned(16))) float rows[kWaves][kMaxRow];
+                                                  int64_t out_plane, int mode, const float* __restrict__ filt,
+                                                  int nstrips, int nchunks, int R, int64_t total_waves, WamNoise nz) {
+  constexpr int p = L - 2;
+  __shared__ __attribute__((aligned(16))) float rows[kWaves][kRowLds];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int64_t gw = (int64_t)blockIdx.x * kWaves + wv;
@@ -165,34 +189,37 @@ __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, 
   }
   const float* src = in + src_plane * in_plane;
   float* lds = rows[wv];
+  const PadLane pl = pad_lane(lane, nw, p, mode);
+  const bool zero_mode = mode == WAM_MODE_ZERO;
+  if (zero_mode && pl.dst >= 0) lds[pl.dst] = 0.f;  // zero pads never change
   const int j0 = strip * 64 * CPL;
   const int i0 = chunk * R;
   const int i1 = min(mh, i0 + R);
   const int er0 = 2 * i0 - p;
 
-  RowRegs<VEC> f[2];
-  constexpr int NZ = NOISE ? RowRegs<VEC>::MAXV * VEC : 1;
+  RowRegs<VEC, MAXV> f[2];
+  constexpr int NZ = NOISE ? 4 * MAXV : 1;
   float nzv[2][NZ];
-  auto fetch = [&](RowRegs<VEC>& r, float (&nzr)[NZ], int er) {
-    const int sr = wam_ext_index(er, nh, mode);
-    r.fetch(src + (int64_t)(sr < 0 ? 0 : sr) * nw, nw, lane, sr >= 0);
-    if constexpr (NOISE) {
-      // an out-of-range (zero) row of 'zero' mode carries no noise: the reference pads noisy_x
-      if (sr >= 0) r.make_noise(nzr, nw, lane, (ch * nh + sr) * (int64_t)nw, sg, img, smp, nz.k0, nz.k1);
-      else
-        for (int u = 0; u < NZ; ++u) nzr[u] = 0.f;
-    }
+  auto fetch = [&](RowRegs<VEC, MAXV>& r, float (&nzr)[NZ], int er) {
+    const int sr = row_src(er, nh, mode);
+    const bool valid = sr >= 0;
+    const int rr = valid ? sr : 0;
+    r.fetch(src + (int64_t)rr * nw, nw, lane, valid);
+    if constexpr (NOISE) make_noise<MAXV>(nzr, nw, lane, (ch * nh + rr) * (int64_t)nw, sg, img, smp, nz.k0, nz.k1, valid);
   };
-  auto process = [&](const RowRegs<VEC>& r, const float (&nzr)[NZ], float (&lo)[CPL], float (&hi)[CPL]) {
-    r.commit(lds, nw, lane, NOISE ? nzr : nullptr);
-    wave_sync();
+  auto process = [&](const RowRegs<VEC, MAXV>& r, const float (&nzr)[NZ], float (&lo)[CPL], float (&hi)[CPL]) {
+    r.commit(lds, lane, NOISE ? nzr : nullptr);
+    wsync();
+    if (!zero_mode) {
+      refresh_pads(lds, pl);
+      wsync();
+    }
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-      const int j = j0 + lane + 64 * c;
-      if (j < mw) hfilter<L>(lds, j, nw, p, mode, flo, fhi, lo[c], hi[c]);
-      else lo[c] = hi[c] = 0.f;
+      const int j = min(j0 + lane + 64 * c, mw - 1);  // clamp: the extra lanes compute a duplicate
+      hfilter<L>(lds, j, p, flo, fhi, lo[c], hi[c]);
     }
-    wave_sync();
+    wsync();
   };
 
   float rl[CPL][L], rh[CPL][L];
@@ -219,7 +246,7 @@ __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, 
       rl[c][L - 2] = lo[c];
       rh[c][L - 2] = hi[c];
     }
-    if (i + 1 < i1) fetch(f[0], nzv[0], er + 2);
+    fetch(f[0], nzv[0], er + 2);  // one row past the chunk on the last iteration: harmless (clamped)
     process(f[1], nzv[1], lo, hi);
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
@@ -266,12 +293,13 @@ struct MapsArgs {
   int64_t full_items;
 };
 
-template <int L, int C, int VEC>
+template <int L, int C, int VEC, int MAXV>
 __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, int nh, int nw, int64_t in_plane,
                                                   float* __restrict__ ll_out, int mh, int mw,
                                                   const float* __restrict__ filt, int nstrips, int nchunks, int R,
                                                   int64_t total_waves, MapsArgs ma) {
-  __shared__ __attribute__((aligned(16))) float rows[kWaves][C][kMaxRow];
+  constexpr int p = L - 2;
+  __shared__ __attribute__((aligned(16))) float rows[kWaves][C][kRowLds];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int64_t gw = (int64_t)blockIdx.x * kWaves + wv;
@@ -280,7 +308,6 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
   const int64_t t = gw / nchunks;
   const int strip = (int)(t % nstrips);
   const int64_t img = t / nstrips;
-  constexpr int p = L - 2;
 
   float flo[L], fhi[L];
 #pragma unroll
@@ -289,29 +316,35 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
     fhi[k] = filt[L + k];
   }
   const float* src = in + img * C * in_plane;
+  {
+    const PadLane pl = pad_lane(lane, nw, p, WAM_MODE_ZERO);
+    if (pl.dst >= 0) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) rows[wv][c][pl.dst] = 0.f;
+    }
+  }
   const int j = strip * 64 + lane;
   const bool jv = j < mw;
+  const int jc = jv ? j : mw - 1;
   const int i0 = chunk * R;
   const int i1 = min(mh, i0 + R);
   const int er0 = 2 * i0 - p;
   const int64_t out_plane = (int64_t)mh * mw;
 
-  RowRegs<VEC> f[2][C];
-  auto fetch = [&](RowRegs<VEC> (&r)[C], int er) {
+  RowRegs<VEC, MAXV> f[2][C];
+  auto fetch = [&](RowRegs<VEC, MAXV> (&r)[C], int er) {
     const bool valid = er >= 0 && er < nh;  // zero padding
+    const int rr = valid ? er : 0;
 #pragma unroll
-    for (int c = 0; c < C; ++c) r[c].fetch(src + c * in_plane + (int64_t)(valid ? er : 0) * nw, nw, lane, valid);
+    for (int c = 0; c < C; ++c) r[c].fetch(src + c * in_plane + (int64_t)rr * nw, nw, lane, valid);
   };
-  auto process = [&](const RowRegs<VEC> (&r)[C], float (&lo)[C], float (&hi)[C]) {
+  auto process = [&](const RowRegs<VEC, MAXV> (&r)[C], float (&lo)[C], float (&hi)[C]) {
 #pragma unroll
-    for (int c = 0; c < C; ++c) r[c].commit(rows[wv][c], nw, lane);
-    wave_sync();
+    for (int c = 0; c < C; ++c) r[c].commit(rows[wv][c], lane, nullptr);
+    wsync();
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      if (jv) hfilter<L>(rows[wv][c], j, nw, p, WAM_MODE_ZERO, flo, fhi, lo[c], hi[c]);
-      else lo[c] = hi[c] = 0.f;
-    }
-    wave_sync();
+    for (int c = 0; c < C; ++c) hfilter<L>(rows[wv][c], jc, p, flo, fhi, lo[c], hi[c]);
+    wsync();
   };
 
   float rl[C][L], rh[C][L];
@@ -340,7 +373,7 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
       rl[c][L - 2] = lo[c];
       rh[c][L - 2] = hi[c];
     }
-    if (i + 1 < i1) fetch(f[0], er + 2);
+    fetch(f[0], er + 2);
     process(f[1], lo, hi);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
@@ -370,17 +403,10 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
         }
       }
       // numpy float32 mean over the channel axis: sequential sum, then true_divide
-      if (c == 0) {
-        sa = a;
-        sh = h;
-        sv = v;
-        sd = d;
-      } else {
-        sa = sa + a;
-        sh = sh + h;
-        sv = sv + v;
-        sd = sd + d;
-      }
+      sa = c == 0 ? a : sa + a;
+      sh = c == 0 ? h : sh + h;
+      sv = c == 0 ? v : sv + v;
+      sd = c == 0 ? d : sd + d;
 #pragma unroll
       for (int k = 0; k < L - 2; ++k) {
         rl[c][k] = rl[c][k + 2];
@@ -419,18 +445,18 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
 }
 
 // ------------------------------------------------------------------------------------------------
-constexpr int64_t kTargetWaves = 4096;
+constexpr int64_t kTargetWaves = 8192;
 
 void pick_chunks(int64_t base, int mh, int& nchunks, int& R) {
   int64_t want = (kTargetWaves + base - 1) / base;
-  int maxchunks = (mh + 15) / 16;  // keep >= 16 output rows per chunk (halo L-2 rows per chunk)
+  int maxchunks = (mh + 11) / 12;  // >= 12 output rows per chunk (L-2 halo rows per chunk)
   if (maxchunks < 1) maxchunks = 1;
   nchunks = (int)(want < 1 ? 1 : (want > maxchunks ? maxchunks : want));
   R = (mh + nchunks - 1) / nchunks;
   nchunks = (mh + R - 1) / R;
 }
 
-template <int L, int CPL, int VEC, bool NOISE>
+template <int L, int CPL, int VEC, int MAXV, bool NOISE>
 int launch_ana_rows_t(int64_t batch, const float* in, int nh, int nw, int mh, int mw, int mode, const float* filt,
                       float* oa, float* oh, float* ov, float* od, const WamNoise* nz, hipStream_t st) {
   const int nstrips = (mw + 64 * CPL - 1) / (64 * CPL);
@@ -440,31 +466,40 @@ int launch_ana_rows_t(int64_t batch, const float* in, int nh, int nw, int mh, in
   WamNoise z = nz ? *nz : WamNoise{nullptr, 1, 1, 0, 0, 0};
   double bytes = 4.0 * ((double)batch * 4.0 * mh * mw + (nz ? (double)z.images * z.channels : (double)batch) * nh * nw);
   WamTimer tm(st, NOISE ? "k_ana_rows<noise>" : "k_ana_rows", bytes);
-  hipLaunchKernelGGL((k_ana_rows<L, CPL, VEC, NOISE>), dim3((unsigned)((waves + kWaves - 1) / kWaves)), dim3(256), 0,
-                     st, in, nh, nw, (int64_t)nh * nw, oa, oh, ov, od, mh, mw, (int64_t)mh * mw, L - 2, mode, filt,
-                     nstrips, nchunks, R, waves, z);
+  hipLaunchKernelGGL((k_ana_rows<L, CPL, VEC, MAXV, NOISE>), dim3((unsigned)((waves + kWaves - 1) / kWaves)),
+                     dim3(256), 0, st, in, nh, nw, (int64_t)nh * nw, oa, oh, ov, od, mh, mw, (int64_t)mh * mw, mode,
+                     filt, nstrips, nchunks, R, waves, z);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
+}
+
+template <int L, int CPL>
+int dispatch_ana_cpl(int64_t batch, const float* in, int nh, int nw, int mh, int mw, int mode, const float* filt,
+                     float* oa, float* oh, float* ov, float* od, const WamNoise* nz, hipStream_t st) {
+  const bool vec4 = (nw % 4 == 0) && ((uintptr_t)in % 16 == 0);
+  if (nz) {
+    if (!vec4) return WAM_ERR_UNSUPPORTED;
+    return nw <= 256 ? launch_ana_rows_t<L, CPL, 4, 1, true>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st)
+                     : launch_ana_rows_t<L, CPL, 4, 2, true>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
+  }
+  if (vec4)
+    return nw <= 256
+               ? launch_ana_rows_t<L, CPL, 4, 1, false>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nullptr, st)
+               : launch_ana_rows_t<L, CPL, 4, 2, false>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nullptr,
+                                                        st);
+  return nw <= 128
+             ? launch_ana_rows_t<L, CPL, 1, 2, false>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nullptr, st)
+             : launch_ana_rows_t<L, CPL, 1, 8, false>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nullptr, st);
 }
 
 template <int L>
 int dispatch_ana(int64_t batch, const float* in, int nh, int nw, int mh, int mw, int mode, const float* filt,
                  float* oa, float* oh, float* ov, float* od, const WamNoise* nz, hipStream_t st) {
-  const bool vec4 = (nw % 4 == 0) && ((uintptr_t)in % 16 == 0);
-  const bool cpl2 = mw > 64;
-  if (nz) {
-    if (!vec4) return WAM_ERR_UNSUPPORTED;
-    return cpl2 ? launch_ana_rows_t<L, 2, 4, true>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st)
-                : launch_ana_rows_t<L, 1, 4, true>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
-  }
-  if (vec4)
-    return cpl2 ? launch_ana_rows_t<L, 2, 4, false>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nullptr, st)
-                : launch_ana_rows_t<L, 1, 4, false>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nullptr, st);
-  return cpl2 ? launch_ana_rows_t<L, 2, 1, false>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nullptr, st)
-              : launch_ana_rows_t<L, 1, 1, false>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nullptr, st);
+  if (mw > 64) return dispatch_ana_cpl<L, 2>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
+  return dispatch_ana_cpl<L, 1>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
 }
 
-template <int L, int C>
+template <int L, int C, int VEC, int MAXV>
 int launch_adj_t(int64_t images, const float* in, int nh, int nw, int mh, int mw, const float* filt, float* ll_out,
                  const MapsArgs& ma, hipStream_t st) {
   const int nstrips = (mw + 63) / 64;
@@ -475,22 +510,28 @@ int launch_adj_t(int64_t images, const float* in, int nh, int nw, int mh, int mw
   double bytes = 4.0 * (double)images * ((double)C * nh * nw + 4.0 * mh * mw + (last ? 0.0 : (double)C * mh * mw) +
                                          (ma.full ? (double)C * 4 * mh * mw : 0.0));
   WamTimer tm(st, "k_adj_maps", bytes);
-  const bool vec4 = (nw % 4 == 0) && ((uintptr_t)in % 16 == 0);
-  if (vec4)
-    hipLaunchKernelGGL((k_adj_maps<L, C, 4>), dim3((unsigned)((waves + kWaves - 1) / kWaves)), dim3(256), 0, st, in,
-                       nh, nw, (int64_t)nh * nw, ll_out, mh, mw, filt, nstrips, nchunks, R, waves, ma);
-  else
-    hipLaunchKernelGGL((k_adj_maps<L, C, 1>), dim3((unsigned)((waves + kWaves - 1) / kWaves)), dim3(256), 0, st, in,
-                       nh, nw, (int64_t)nh * nw, ll_out, mh, mw, filt, nstrips, nchunks, R, waves, ma);
+  hipLaunchKernelGGL((k_adj_maps<L, C, VEC, MAXV>), dim3((unsigned)((waves + kWaves - 1) / kWaves)), dim3(256), 0, st,
+                     in, nh, nw, (int64_t)nh * nw, ll_out, mh, mw, filt, nstrips, nchunks, R, waves, ma);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
+}
+
+template <int L, int C>
+int dispatch_adj_c(int64_t images, const float* in, int nh, int nw, int mh, int mw, const float* filt, float* ll_out,
+                   const MapsArgs& ma, hipStream_t st) {
+  const bool vec4 = (nw % 4 == 0) && ((uintptr_t)in % 16 == 0);
+  if (vec4)
+    return nw <= 256 ? launch_adj_t<L, C, 4, 1>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st)
+                     : launch_adj_t<L, C, 4, 2>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+  return nw <= 128 ? launch_adj_t<L, C, 1, 2>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st)
+                   : launch_adj_t<L, C, 1, 8>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
 }
 
 template <int L>
 int dispatch_adj(int channels, int64_t images, const float* in, int nh, int nw, int mh, int mw, const float* filt,
                  float* ll_out, const MapsArgs& ma, hipStream_t st) {
-  if (channels == 3) return launch_adj_t<L, 3>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
-  if (channels == 1) return launch_adj_t<L, 1>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+  if (channels == 3) return dispatch_adj_c<L, 3>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+  if (channels == 1) return dispatch_adj_c<L, 1>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
   return WAM_ERR_UNSUPPORTED;
 }
 
@@ -501,7 +542,7 @@ bool l_supported(int L) { return L == 2 || L == 4 || L == 6 || L == 8 || L == 12
 bool dwt2_rows_supported(const wam_plan* p, int level, bool adjoint) {
   if (p->ndim != 2 || !l_supported(p->L)) return false;
   const int64_t nw = (adjoint && level == 0) ? p->rec_shape[1] : p->lin[level][1];
-  return nw <= kMaxRow && nw >= 1;
+  return nw <= kMaxRow && nw >= 4;
 }
 
 int launch_dwt2_analysis_rows(const wam_plan* p, int64_t batch, const float* in, const int64_t* in_dims,
