@@ -50,8 +50,9 @@ int wam_version(void);
 int wam_plan_create(wam_plan** plan, int ndim, const int64_t* shape, int levels,
                     const double* dec_lo, const double* dec_hi,
                     const double* rec_lo, const double* rec_hi, int filt_len, int mode);
-/* flags: WAM_PLAN_GENERIC forces the per-axis kernels (used by tests to cross-check the fused
- * 2D kernels); 0 selects the fastest path. wam_plan_create == wam_plan_create_ex(..., 0). */
+/* flags: WAM_PLAN_GENERIC forces the per-axis kernels, WAM_PLAN_NO_ROWS skips the row-resident
+ * 2D kernels (both used by tests to cross-check the fused 2D kernels); 0 selects the fastest
+ * path. wam_plan_create == wam_plan_create_ex(..., 0). */
 enum wam_plan_flags { WAM_PLAN_GENERIC = 1, WAM_PLAN_NO_ROWS = 2 };
 int wam_plan_create_ex(wam_plan** plan, int ndim, const int64_t* shape, int levels,
                        const double* dec_lo, const double* dec_hi,

@@ -192,9 +192,12 @@ def test_matlab_known_answers(wam):
 # ------------------------------------------------------------------------------ fused WAM passes
 @pytest.mark.parametrize("wav,shape,J,mode", [("db4", (224, 224), 3, "reflect"), ("haar", (224, 224), 3, "zero"),
                                               ("sym8", (96, 128), 2, "symmetric"), ("db6", (60, 44), 2, "constant"),
-                                              ("haar", (512, 512), 5, "periodic")])
-def test_rows_colstrip_generic_agree(wam, wav, shape, J, mode):
-    """The three 2D analysis implementations (row-resident, column-strip, per-axis) agree."""
+                                              ("haar", (512, 512), 5, "periodic"), ("db4", (37, 53), 2, "reflect"),
+                                              ("sym4", (300, 700), 3, "symmetric"), ("db10", (33, 260), 1, "zero"),
+                                              ("coif1", (7, 9), 1, "periodic")])
+def test_fused_2d_paths_agree(wam, wav, shape, J, mode):
+    """The 2D analysis implementations (row-resident, column-strip, per-axis) agree: bit-exact
+    between the fused kernels (same tap order), to fp32 rounding with the per-axis one."""
     torch.manual_seed(5)
     B = 6
     x = torch.randn((B,) + shape, device="cuda")
@@ -225,7 +228,8 @@ def test_noisy_wavedec_equals_noise_then_wavedec(wam, wav, J):
 
 
 @pytest.mark.parametrize("wav,shape,J,C", [("db4", (224, 224), 3, 3), ("haar", (224, 224), 3, 3),
-                                           ("sym8", (128, 96), 2, 1), ("db6", (225, 223), 3, 3)])
+                                           ("sym8", (128, 96), 2, 1), ("db6", (225, 223), 3, 3),
+                                           ("db2", (64, 300), 2, 1)])
 def test_adjoint_maps_equals_adjoint_then_subband_maps(wam, wav, shape, J, C):
     p = wam.get_plan(2, shape, J, wav, "reflect", "cuda")
     assert p.caps & wam.CAP_ADJOINT_MAPS

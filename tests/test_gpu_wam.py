@@ -133,6 +133,22 @@ def test_philox_noise_statistics(W):
     assert not torch.equal(a[0], a[1])
 
 
+def test_philox_stream_matches_host_restatement(W):
+    """The GPU noise stream is Philox4x32-10 (pinned by the Random123 known answers on the host
+    restatement, tests/test_host_logic.py) + Box-Muller on the hardware transcendentals: compare
+    every drawn value with the float64 host restatement (|err| <= 2e-5 * (1 + |z|))."""
+    from wam_amd import plan as P
+    from tests.helpers import philox_normals
+    n, items, samples, base, seed = 4099, 3, 2, 5, 0x1234_5678_9ABC
+    x = torch.zeros(items, n, device="cuda")
+    sigma = torch.ones(items, device="cuda")
+    z = P.noise_add(x, sigma, samples, items, n, n, seed=seed, sample_base=base).view(samples, items, n).cpu().numpy()
+    for s in range(samples):
+        for i in range(items):
+            ref = philox_normals(n, i, base + s, seed)
+            assert np.all(np.abs(z[s, i] - ref) <= 2e-5 * (1 + np.abs(ref))), (s, i)
+
+
 def test_resnet18_c1_statistical(W):
     """Config c1 (haar J=3 SmoothGrad n=25, random-init ResNet-18, 1 image, numpy noise) vs the
     oracle on this box's CPU. ReLU kinks make the map sensitive to fp32 rounding (a

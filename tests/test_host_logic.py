@@ -138,3 +138,15 @@ def test_auto_group():
     assert engine.auto_group(m, 1, None) == 256
     assert engine.auto_group(m.train(), 64, None) == 1
     assert engine.auto_group(m, 64, 3) == 3
+
+
+def test_philox_known_answers():
+    """Random123 known-answer vectors for Philox4x32-10 (the host restatement of rng.hpp)."""
+    from tests.helpers import philox4x32_10
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((0xffffffff,) * 4, (0xffffffff, 0xffffffff), (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for ctr, key, want in kat:
+        got = philox4x32_10(*[np.array([v]) for v in ctr], *key)
+        assert tuple(int(v[0]) for v in got) == want

@@ -72,7 +72,7 @@ struct RowRegs {
   }
 
   // commit to the padded LDS row (sample s at lds[kPadL + s]); noise (optional) added here
-  __device__ __forceinline__ void commit(float* lds, int lane, const float* nz) const {
+  __device__ __forceinline__ void commit(float* lds, int lane, const float* nz, float sg = 0.f) const {
 #pragma unroll
     for (int q = 0; q < MAXV; ++q) {
       const int idx = (lane + 64 * q) * VEC;
@@ -80,10 +80,11 @@ struct RowRegs {
         float4 o = ok[q] ? make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3])
                          : make_float4(0.f, 0.f, 0.f, 0.f);
         if (nz) {
-          o.x += nz[4 * q];
-          o.y += nz[4 * q + 1];
-          o.z += nz[4 * q + 2];
-          o.w += nz[4 * q + 3];
+          // noisy = fma(sigma, z, x): the same rounding as wam_noise_add
+          o.x = fmaf(sg, nz[4 * q], o.x);
+          o.y = fmaf(sg, nz[4 * q + 1], o.y);
+          o.z = fmaf(sg, nz[4 * q + 2], o.z);
+          o.w = fmaf(sg, nz[4 * q + 3], o.w);
         }
         *reinterpret_cast<float4*>(lds + kPadL + idx) = o;
       } else {
@@ -104,7 +105,7 @@ __device__ __forceinline__ void make_noise(float (&nz)[4 * MAXV], int nw, int la
     wam_normal4((row_elem0 + (idx < nw ? idx : 0)) >> 2, img, smp, k0, k1, z);
     const bool ok = valid && idx < nw;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) nz[4 * q + u] = ok ? sg * z[u] : 0.f;
+    for (int u = 0; u < 4; ++u) nz[4 * q + u] = ok ? z[u] : 0.f;
   }
 }
 
@@ -208,7 +209,7 @@ __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, 
     if constexpr (NOISE) make_noise<MAXV>(nzr, nw, lane, (ch * nh + rr) * (int64_t)nw, sg, img, smp, nz.k0, nz.k1, valid);
   };
   auto process = [&](const RowRegs<VEC, MAXV>& r, const float (&nzr)[NZ], float (&lo)[CPL], float (&hi)[CPL]) {
-    r.commit(lds, lane, NOISE ? nzr : nullptr);
+    r.commit(lds, lane, NOISE ? nzr : nullptr, sg);
     wsync();
     if (!zero_mode) {
       refresh_pads(lds, pl);

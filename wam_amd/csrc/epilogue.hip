@@ -11,34 +11,51 @@
 
 namespace {
 
-// ------------------------------------------------------------------------------ wave reductions
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
 // numpy-compatible max: NaN propagates (fmaxf would drop it)
 __device__ __forceinline__ float nan_max(float a, float b) { return (a != a || a > b) ? a : b; }
 
 // ------------------------------------------------------------------------------ sigma
-__global__ void __launch_bounds__(256) k_item_sigma(const float* __restrict__ x, int64_t item_stride, int64_t len,
-                                                    float spread, float* __restrict__ sigma) {
+__device__ __forceinline__ float nan_min(float a, float b) { return (a != a || a < b) ? a : b; }
+
+// One 1024-thread block per item; VEC4 streams 16-byte loads, 4 in flight per thread.
+// max/min propagate NaN like torch.max / torch.min.
+template <bool VEC4>
+__global__ void __launch_bounds__(1024) k_item_sigma(const float* __restrict__ x, int64_t item_stride, int64_t len,
+                                                     float spread, float* __restrict__ sigma) {
   const float* xi = x + blockIdx.x * item_stride;
   float mx = -INFINITY, mn = INFINITY;
-  for (int64_t e = threadIdx.x; e < len; e += blockDim.x) {
-    float v = xi[e];
-    mx = fmaxf(mx, v);
-    mn = fminf(mn, v);
+  if constexpr (VEC4) {
+    const float4* x4 = reinterpret_cast<const float4*>(xi);
+    const int64_t n4 = len >> 2;
+    int64_t e = threadIdx.x;
+    for (; e + 3 * 1024 < n4; e += 4 * 1024) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = x4[e + u * 1024];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        mx = nan_max(nan_max(mx, v[u].x), nan_max(nan_max(v[u].y, v[u].z), v[u].w));
+        mn = nan_min(nan_min(mn, v[u].x), nan_min(nan_min(v[u].y, v[u].z), v[u].w));
+      }
+    }
+    for (; e < n4; e += 1024) {
+      const float4 v = x4[e];
+      mx = nan_max(nan_max(mx, v.x), nan_max(nan_max(v.y, v.z), v.w));
+      mn = nan_min(nan_min(mn, v.x), nan_min(nan_min(v.y, v.z), v.w));
+    }
+  } else {
+    for (int64_t e = threadIdx.x; e < len; e += 1024) {
+      const float v = xi[e];
+      mx = nan_max(mx, v);
+      mn = nan_min(mn, v);
+    }
   }
-  mx = wave_max(mx);
-  mn = wave_min(mn);
-  __shared__ float smx[4], smn[4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = nan_max(mx, __shfl_xor(mx, o, 64));
+    mn = nan_min(mn, __shfl_xor(mn, o, 64));
+  }
+  __shared__ float smx[16], smn[16];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (lane == 0) {
     smx[wv] = mx;
@@ -46,9 +63,9 @@ __global__ void __launch_bounds__(256) k_item_sigma(const float* __restrict__ x,
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
-      mx = fmaxf(mx, smx[w]);
-      mn = fminf(mn, smn[w]);
+    for (int w = 1; w < 16; ++w) {
+      mx = nan_max(mx, smx[w]);
+      mn = nan_min(mn, smn[w]);
     }
     // torch: spread * (max - min) in fp32 with the python scalar cast to fp32
     sigma[blockIdx.x] = spread * (mx - mn);
@@ -79,10 +96,14 @@ __global__ void __launch_bounds__(256) k_noise_add(int64_t n_samples, int64_t it
     const float* hn = host_noise ? host_noise + (s * items + i) * item_stride : nullptr;
     if (VEC4 && 4 * g + 4 <= noised_len) {
       float4 xv = *reinterpret_cast<const float4*>(xi + 4 * g);
-      float4 nv;
-      if (hn) nv = *reinterpret_cast<const float4*>(hn + 4 * g);
-      else nv = make_float4(sg * z[0], sg * z[1], sg * z[2], sg * z[3]);
-      *reinterpret_cast<float4*>(oi + 4 * g) = make_float4(xv.x + nv.x, xv.y + nv.y, xv.z + nv.z, xv.w + nv.w);
+      float4 o;
+      if (hn) {
+        float4 nv = *reinterpret_cast<const float4*>(hn + 4 * g);
+        o = make_float4(xv.x + nv.x, xv.y + nv.y, xv.z + nv.z, xv.w + nv.w);
+      } else {  // noisy = fma(sigma, z, x): the same rounding as the fused noisy analysis
+        o = make_float4(fmaf(sg, z[0], xv.x), fmaf(sg, z[1], xv.y), fmaf(sg, z[2], xv.z), fmaf(sg, z[3], xv.w));
+      }
+      *reinterpret_cast<float4*>(oi + 4 * g) = o;
       continue;
     }
 #pragma unroll
@@ -90,7 +111,7 @@ __global__ void __launch_bounds__(256) k_noise_add(int64_t n_samples, int64_t it
       int64_t e = 4 * g + u;
       if (e >= item_stride) break;
       float v;
-      if (e < noised_len) v = xi[e] + (hn ? hn[e] : sg * z[u]);
+      if (e < noised_len) v = hn ? xi[e] + hn[e] : fmaf(sg, z[u], xi[e]);
       else v = 0.f;
       oi[e] = v;
     }
@@ -337,8 +358,14 @@ int wam_item_sigma(int64_t items, int64_t item_stride, int64_t len, const float*
                    void* stream) {
   if (items < 0 || len < 1 || !x || !sigma) return WAM_ERR_INVALID_ARG;
   if (items == 0) return WAM_OK;
-  hipLaunchKernelGGL(k_item_sigma, dim3((unsigned)items), dim3(256), 0, (hipStream_t)stream, x, item_stride, len, spread,
-                     sigma);
+  const bool vec4 = item_stride % 4 == 0 && len % 4 == 0 && (uintptr_t)x % 16 == 0;
+  WamTimer tm((hipStream_t)stream, "k_item_sigma", 4.0 * (double)items * len);
+  if (vec4)
+    hipLaunchKernelGGL(k_item_sigma<true>, dim3((unsigned)items), dim3(1024), 0, (hipStream_t)stream, x, item_stride,
+                       len, spread, sigma);
+  else
+    hipLaunchKernelGGL(k_item_sigma<false>, dim3((unsigned)items), dim3(1024), 0, (hipStream_t)stream, x, item_stride,
+                       len, spread, sigma);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }

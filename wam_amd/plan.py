@@ -14,35 +14,6 @@ _CACHE = {}
 _LOCK = threading.Lock()
 PLAN_GENERIC = 1
 
-# Optional live timing of the transform entry points (bench.py): op -> list of
-# (start event, end event, algorithmic bytes). Events are recorded on the stream the kernels run on.
-_PROFILE = None
-
-
-def set_profile(store):
-    """store: dict to collect events into, or None to disable."""
-    global _PROFILE
-    _PROFILE = store
-
-
-class _timed:
-    def __init__(self, op, device, nbytes):
-        self.op, self.device, self.nbytes = op, device, nbytes
-
-    def __enter__(self):
-        if _PROFILE is not None:
-            self.s = torch.cuda.Event(enable_timing=True)
-            self.e = torch.cuda.Event(enable_timing=True)
-            self.s.record(torch.cuda.current_stream(self.device))
-        return self
-
-    def __exit__(self, *a):
-        if _PROFILE is not None:
-            self.e.record(torch.cuda.current_stream(self.device))
-            _PROFILE.setdefault(self.op, []).append((self.s, self.e, self.nbytes))
-        return False
-
-
 class Plan:
     """Immutable transform plan (ndim, spatial shape, levels, wavelet, mode) on one device."""
 
@@ -123,8 +94,7 @@ class Plan:
         if out is None:
             out = torch.empty(batch * self.coeff_numel, dtype=torch.float32, device=x.device)
         ws = self.workspace(batch)
-        with _timed("wavedec", x.device, 4 * batch * (int(np.prod(self.shape)) + self.coeff_numel)):
-            check(lib.wam_wavedec(self._h, batch, ptr(x), ptr(out), ptr(ws), stream_of(x.device)))
+        check(lib.wam_wavedec(self._h, batch, ptr(x), ptr(out), ptr(ws), stream_of(x.device)))
         return out
 
     def waverec(self, flat, batch, alphas=None, out=None):
@@ -135,10 +105,8 @@ class Plan:
         if out is None:
             out = torch.empty((n_alpha, batch) + self.rec_shape, dtype=torch.float32, device=flat.device)
         ws = self.workspace(batch)
-        nbytes = 4 * batch * (self.coeff_numel + n_alpha * int(np.prod(self.rec_shape)))
-        with _timed("waverec", flat.device, nbytes):
-            check(lib.wam_waverec(self._h, batch, ptr(flat.contiguous()), a, n_alpha, ptr(out), ptr(ws),
-                                  stream_of(flat.device)))
+        check(lib.wam_waverec(self._h, batch, ptr(flat.contiguous()), a, n_alpha, ptr(out), ptr(ws),
+                              stream_of(flat.device)))
         return out
 
     def adjoint(self, grad, out=None):
@@ -149,8 +117,7 @@ class Plan:
         if out is None:
             out = torch.empty(batch * self.coeff_numel, dtype=torch.float32, device=grad.device)
         ws = self.workspace(batch)
-        with _timed("adjoint", grad.device, 4 * batch * (int(np.prod(self.rec_shape)) + self.coeff_numel)):
-            check(lib.wam_waverec_adjoint(self._h, batch, ptr(grad), ptr(out), ptr(ws), stream_of(grad.device)))
+        check(lib.wam_waverec_adjoint(self._h, batch, ptr(grad), ptr(out), ptr(ws), stream_of(grad.device)))
         return out
 
     # ---------------------------------------------------------------- fused WAM passes
@@ -237,10 +204,9 @@ def item_sigma(x, item_stride, length, spread):
 def noise_add(x, sigma, n_samples, items, item_stride, noised_len, seed=0, sample_base=0, host_noise=None, out=None):
     if out is None:
         out = torch.empty((n_samples * items * item_stride,), dtype=torch.float32, device=x.device)
-    with _timed("noise_add", x.device, 4 * items * item_stride * (1 + n_samples)):
-        check(lib.wam_noise_add(n_samples, items, item_stride, noised_len, ptr(x), ptr(sigma), ptr(host_noise),
-                                ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), sample_base, ptr(out),
-                                stream_of(x.device)))
+    check(lib.wam_noise_add(n_samples, items, item_stride, noised_len, ptr(x), ptr(sigma), ptr(host_noise),
+                            ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), sample_base, ptr(out),
+                            stream_of(x.device)))
     return out
 
 
@@ -253,19 +219,16 @@ def subband_maps(plan, coeff_grads, groups, group_items, channels, maps=None, ba
         band_max = torch.zeros((groups, plan.nbands), dtype=torch.float32, device=dev)
     else:
         band_max.zero_()
-    with _timed("subband_maps", dev, 4 * items * (channels + 1) * plan.coeff_numel):
-        check(lib.wam_subband_maps(plan.handle, groups, group_items, channels, ptr(coeff_grads), ptr(maps),
-                                   ptr(band_max), stream_of(dev)))
+    check(lib.wam_subband_maps(plan.handle, groups, group_items, channels, ptr(coeff_grads), ptr(maps),
+                               ptr(band_max), stream_of(dev)))
     return maps, band_max
 
 
 def frame_accumulate(groups, group_items, gmap, maps, maps_item_len, band_max, n_bands, normalize, frame):
     src, band = gmap
-    nbytes = 4 * groups * group_items * maps_item_len + 16 * group_items * src.numel()
-    with _timed("frame_accumulate", frame.device, nbytes):
-        check(lib.wam_frame_accumulate(groups, group_items, src.numel(), ptr(src), ptr(band), ptr(maps),
-                                       maps_item_len, ptr(band_max), n_bands, int(bool(normalize)), ptr(frame),
-                                       stream_of(frame.device)))
+    check(lib.wam_frame_accumulate(groups, group_items, src.numel(), ptr(src), ptr(band), ptr(maps),
+                                   maps_item_len, ptr(band_max), n_bands, int(bool(normalize)), ptr(frame),
+                                   stream_of(frame.device)))
 
 
 def frame_trapz(groups, k0, group_items, gmap, maps, maps_item_len, band_max, n_bands, normalize, prev, acc,
