@@ -46,22 +46,32 @@ def main():
     ap.add_argument("--wavelet", default="db4")
     ap.add_argument("--levels", type=int, default=3)
     ap.add_argument("--size", type=int, default=224)
+    ap.add_argument("--samples", type=int, default=25, help="noise samples per WAM launch (bench: all 25)")
     args = ap.parse_args()
     torch.manual_seed(0)
-    N, C, S, H = 64, 3, 4, args.size
+    N, C, S, H = 64, 3, args.samples, args.size
     x = torch.randn(N, C, H, H, device="cuda")
-    for flags, tag in [(0, "rows"), (P.PLAN_NO_ROWS, "colstrip")]:
+    modes = [(0, "plane"), (P.PLAN_NO_PLANE, "rows")]
+    if os.environ.get("KBENCH_PLANE_ONLY"):
+        modes = modes[:1]
+    for flags, tag in modes:
         p = P.get_plan(2, (H, H), args.levels, args.wavelet, "reflect", "cuda", flags=flags)
         sigma = P.item_sigma(x, C * H * H, C * H * H, 0.25)
         if p.caps & P.CAP_NOISY_WAVEDEC:
             run(f"{tag} wavedec_noisy S={S}", lambda: p.wavedec_noisy(x, sigma, S, N, C, seed=1, sample_base=0),
                 args.iters)
+            xb = torch.randn(S * N, C, H, H, device="cuda")
+            sb = P.item_sigma(xb, C * H * H, C * H * H, 0.25)
+            run(f"{tag} wavedec_noisy S=1 N={S * N} (no shared source)",
+                lambda: p.wavedec_noisy(xb, sb, 1, S * N, C, seed=1, sample_base=0), args.iters)
+            del xb
         xs = torch.randn(S * N * C, H, H, device="cuda")
         run(f"{tag} wavedec", lambda: p.wavedec(xs), args.iters)
         g = torch.randn((S * N * C,) + p.rec_shape, device="cuda")
         if p.caps & P.CAP_ADJOINT_MAPS:
             run(f"{tag} adjoint_maps", lambda: p.adjoint_maps(g, S, N, C, full=False), args.iters)
         run(f"{tag} adjoint", lambda: p.adjoint(g), args.iters)
+        del g
         cf = p.wavedec(xs)
         run(f"{tag} waverec", lambda: p.waverec(cf, S * N * C), args.iters)
 

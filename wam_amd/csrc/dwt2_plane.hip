@@ -1,0 +1,495 @@
+// Plane-resident multi-level 2D analysis for gfx950: ALL J levels of one plane in ONE workgroup,
+// the LL pyramid never leaves LDS.
+//
+// Why: the per-level kernels (dwt2_rows.hip) write LL_1 to HBM and read it back for level 2, and
+// every coarse level is its own small launch whose ramp-up dominates (a 224^2 db4 batch spends
+// 45 us in levels 2-3 for 16% of the bytes). Here a 512-thread workgroup owns one plane (or one
+// image of C planes for the WAM backward pass):
+//   phase 1  level 1 (finest), row-resident: each of the 8 waves streams a chunk of whole source
+//            rows with 16-B loads, 3 rows in flight (4-deep register ring of fetched rows), adds
+//            the SmoothGrad noise at commit time (Philox, same stream as wam_noise_add) or
+//            averages the C channel rows (WAM backward: mean over C commutes with the linear
+//            adjoint), applies the boundary extension in LDS pad slots, filters horizontally from
+//            LDS and vertically from a register ring of L rows. H/V/D go to HBM, LL_1 to LDS.
+//   phase 2  levels 2..J from LDS: one thread per output column and row block, horizontal taps
+//            through precomputed extended column indices, vertical register ring; LL ping-pongs
+//            between two LDS buffers, the last level writes A_J.
+// Two workgroups fit a CU for 224^2 inputs (LL_1 53 KB + 9 KB of wave rows), 16 waves per CU.
+//
+// Outputs: coefficient mode = band-major coefficients (as wam_wavedec); maps mode = the WAM
+// epilogue (lib/wam_2D.py:227-256): |coefficient of the channel mean| packed item-major, and
+// per-band maxima reduced wave -> LDS -> one global atomic max per workgroup and band.
+//
+// Workgroup order: an XCD-aware bijective swizzle makes consecutive logical workgroups share an
+// XCD (L2); for noisy analysis the logical order is sample-fastest, so the S noise samples of one
+// clean plane run back to back on one XCD and its rows are read from HBM about once.
+#include <atomic>
+
+#include "rowtools.hpp"
+
+namespace {
+
+using namespace wam_rows;
+
+constexpr int kPW = 8;                 // waves per workgroup
+constexpr int kPT = 64 * kPW;          // threads per workgroup
+constexpr int kPlaneMaxW = 256;        // level-0 row width (one float4 per lane)
+constexpr int kPlaneMaxMW = 128;       // level-1 output width (two columns per lane)
+constexpr int kPlaneLdsCap = 160 * 1024 - 1024;
+
+struct PlaneGeom {
+  int J;
+  int mode;
+  int nh0, nw0;
+  int mh[WAM_MAX_LEVELS], mw[WAM_MAX_LEVELS];
+  int64_t off_a;                    // per-item offset of band 0 (A_J)
+  int64_t off[WAM_MAX_LEVELS][3];   // per-item offsets of (H, V, D) of level l (0 = finest)
+  int band[WAM_MAX_LEVELS][3];      // their band indices
+  int nbands;
+  int64_t items_total;              // band-major multiplier (coefficient mode)
+  int64_t maps_item;                // packed floats per item (maps mode)
+  int rowlds;                       // floats per wave-private row
+  int llcap;                        // floats of LDS buffer A (LL_1, LL_3, ...)
+};
+
+template <bool MAPS>
+struct BandOut {
+  float* out;
+  int64_t item;
+  __device__ __forceinline__ void put(const PlaneGeom& g, int64_t off, int64_t numel, int64_t idx, float v,
+                                      float& mx) const {
+    if constexpr (MAPS) {
+      const float a = fabsf(v);
+      out[item * g.maps_item + off + idx] = a;
+      mx = nan_max(mx, a);
+    } else {
+      out[g.items_total * off + item * numel + idx] = v;
+    }
+  }
+};
+
+__device__ __forceinline__ float wave_max(float m) {
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) m = nan_max(m, __shfl_xor(m, s, 64));
+  return m;
+}
+
+// MC: 0 = one input plane per item; C > 0 = item is an image of C planes, averaged on load
+// CPL: level-1 output columns per lane (mw <= 64 * CPL): one wave covers a whole row
+template <int L, int CPL, bool NOISE, int MC, bool MAPS>
+__global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))) k_plane_ana(const float* __restrict__ in, float* __restrict__ out,
+                                                   float* __restrict__ band_max, const float* __restrict__ filt,
+                                                   PlaneGeom g, WamNoise nz, int64_t n_items, int64_t S,
+                                                   int64_t group_items) {
+  constexpr int p = L - 2;
+  constexpr int NCH = MC > 0 ? MC : 1;
+  // fetched-row ring: NB-1 rows in flight while one is consumed (C channel rows each); sized
+  // so that the kernel stays within 128 VGPRs (16 waves per CU) without spilling
+  constexpr int NB = CPL > 1 ? 2 : (NCH > 1 ? 3 : 4);
+  constexpr int GRP = (NB % 2 == 0) ? NB : 2 * NB;  // rows per steady-state iteration (even)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ unsigned int wg_max[WAM_MAX_BANDS];
+
+  // ---- logical workgroup: bijective XCD swizzle (consecutive logical ids share an XCD)
+  const int64_t nwg = gridDim.x, bid = blockIdx.x;
+  const int64_t q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const int64_t lwg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  if (lwg >= n_items) return;  // never taken (grid == n_items); keeps the barrier count uniform
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nh = g.nh0, nw = g.nw0;
+  const int64_t in_plane = (int64_t)nh * nw;
+
+  int64_t item = lwg, src_plane = lwg, img = 0, smp = 0, ch = 0;
+  float sg = 0.f;
+  if constexpr (NOISE) {
+    const int64_t nc = nz.images * nz.channels;
+    src_plane = lwg / S;                  // sample-fastest: the S samples of a plane are adjacent
+    const int64_t s = lwg % S;
+    item = s * nc + src_plane;            // output planes are (sample, image, channel)
+    smp = nz.sample_base + s;
+    img = src_plane / nz.channels;
+    ch = src_plane % nz.channels;
+    sg = nz.sigma[img];
+  }
+  const float* src = in + src_plane * (int64_t)NCH * in_plane;
+
+  float flo[L], fhi[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    flo[k] = filt[k];
+    fhi[k] = filt[L + k];
+  }
+  if constexpr (MAPS) {
+    if (tid < g.nbands) wg_max[tid] = 0u;
+    __syncthreads();
+  }
+  const BandOut<MAPS> bo{out, item};
+  float* bufA = smem;
+  float* bufB = smem + g.llcap;
+
+  // ================================================================ phase 1: level 1 (finest)
+  {
+    const int mh = g.mh[0], mw = g.mw[0];
+    const int64_t bn = (int64_t)mh * mw;
+    const bool lastlvl = g.J == 1;
+    float* lds = bufB + wv * g.rowlds;
+    const int mode = g.mode;
+    const bool zero_mode = mode == WAM_MODE_ZERO;
+    const PadLane pl = pad_lane(lane, nw, p, mode);
+    if (zero_mode && pl.dst >= 0) lds[pl.dst] = 0.f;
+    const int R = (mh + kPW - 1) / kPW;
+    const int i0 = wv * R;
+    const int i1 = min(mh, i0 + R);
+    const int er0 = 2 * i0 - p;
+    const int T = i1 > i0 ? 2 * (i1 - i0) + L - 2 : 0;
+    float mx[4] = {0.f, 0.f, 0.f, 0.f};
+
+    RowRegs<4, 1> f[NB][NCH];
+    int srow[NB];
+    auto fetch = [&](RowRegs<4, 1> (&fr)[NCH], int& sr_out, int t) {
+      const int sr = row_src(er0 + t, nh, mode);
+      const bool valid = sr >= 0;
+      const int rr = valid ? sr : 0;
+      sr_out = sr;  // -1: zero row
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) fr[c].fetch(src + c * in_plane + (int64_t)rr * nw, nw, lane, valid);
+    };
+    auto consume = [&](RowRegs<4, 1> (&fr)[NCH], int sr, float (&lo)[CPL], float (&hi)[CPL]) {
+      // the noise depends only on (row, lane): generate it before touching the fetched row so the
+      // Philox work overlaps the row's load latency instead of following its vmcnt wait
+      float nzr[4];
+      if constexpr (NOISE)
+        make_noise<1>(nzr, nw, lane, (ch * nh + (sr >= 0 ? sr : 0)) * (int64_t)nw, sg, img, smp, nz.k0, nz.k1,
+                      sr >= 0);
+      RowRegs<4, 1> m = fr[0];
+      if constexpr (NCH > 1) {
+#pragma unroll
+        for (int c = 1; c < NCH; ++c)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) m.v[u] += fr[c].v[u];
+        constexpr float inv = 1.0f / (float)NCH;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) m.v[u] *= inv;
+      }
+      if constexpr (NOISE) {
+        m.commit(lds, lane, nzr, sg);
+      } else {
+        m.commit(lds, lane, nullptr);
+      }
+      wsync();
+      if (!zero_mode) {
+        refresh_pads(lds, pl);
+        wsync();
+      }
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int j = min(lane + 64 * c, mw - 1);
+        hfilter<L>(lds, j, p, flo, fhi, lo[c], hi[c]);
+      }
+      wsync();
+    };
+
+    float rl[CPL][L], rh[CPL][L];
+    auto emit = [&](int i) {
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int j = lane + 64 * c;
+        float a = 0.f, h = 0.f, v = 0.f, d = 0.f;
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+          a = fmaf(flo[k], rl[c][k], a);
+          h = fmaf(fhi[k], rl[c][k], h);
+          v = fmaf(flo[k], rh[c][k], v);
+          d = fmaf(fhi[k], rh[c][k], d);
+        }
+        if (j < mw && i < i1) {
+          const int64_t idx = (int64_t)i * mw + j;
+          if (lastlvl) bo.put(g, g.off_a, bn, idx, a, mx[3]);
+          else bufA[idx] = a;
+          bo.put(g, g.off[0][0], bn, idx, h, mx[0]);
+          bo.put(g, g.off[0][1], bn, idx, v, mx[1]);
+          bo.put(g, g.off[0][2], bn, idx, d, mx[2]);
+        }
+#pragma unroll
+        for (int k = 0; k < L - 2; ++k) {
+          rl[c][k] = rl[c][k + 2];
+          rh[c][k] = rh[c][k + 2];
+        }
+      }
+    };
+
+    // Every fetch is unconditional (rows past the chunk are clamped to valid source rows and never
+    // emitted): loads under divergent control flow would make the compiler drain vmcnt to 0 at the
+    // join, serialising the row stream on memory latency.
+    if (T > 0) {
+#pragma unroll
+      for (int u = 0; u < NB - 1; ++u) fetch(f[u], srow[u], u);
+      // prologue: ext rows 0 .. L-3 fill ring slots 0 .. L-3
+#pragma unroll
+      for (int t = 0; t < L - 2; ++t) {
+        fetch(f[(t + NB - 1) % NB], srow[(t + NB - 1) % NB], t + NB - 1);
+        float lo[CPL], hi[CPL];
+        consume(f[t % NB], srow[t % NB], lo, hi);
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          rl[c][t] = lo[c];
+          rh[c][t] = hi[c];
+        }
+      }
+      // steady state: GRP ext rows (GRP/2 output rows) per iteration, static ring-buffer indices;
+      // a partial last group computes output rows >= i1, which emit() drops
+      for (int base = L - 2; base < T; base += GRP) {
+#pragma unroll
+        for (int u = 0; u < GRP; ++u) {
+          const int t = base + u;
+          const int fb = (L - 2 + u + NB - 1) % NB;
+          fetch(f[fb], srow[fb], t + NB - 1);
+          float lo[CPL], hi[CPL];
+          consume(f[(L - 2 + u) % NB], srow[(L - 2 + u) % NB], lo, hi);
+          const int slot = (u & 1) ? L - 1 : L - 2;
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) {
+            rl[c][slot] = lo[c];
+            rh[c][slot] = hi[c];
+          }
+          if (u & 1) emit(i0 + (t - (L - 1)) / 2);
+        }
+      }
+    }
+    if constexpr (MAPS) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mx[b] = wave_max(mx[b]);
+      if (lane == 0) {
+#pragma unroll
+        for (int b = 0; b < 3; ++b) atomicMax(&wg_max[g.band[0][b]], __float_as_uint(mx[b]));
+        if (lastlvl) atomicMax(&wg_max[0], __float_as_uint(mx[3]));
+      }
+    }
+  }
+
+  // ================================================================ phase 2: levels 2..J in LDS
+  const float* lsrc = bufA;
+  float* ldst = bufB;
+  for (int l = 1; l < g.J; ++l) {
+    __syncthreads();  // LL_l complete in lsrc; the buffer ldst is free
+    const int sh = g.mh[l - 1], sw = g.mw[l - 1], mh = g.mh[l], mw = g.mw[l];
+    const int64_t bn = (int64_t)mh * mw;
+    const bool lastlvl = l == g.J - 1;
+    const int mode = g.mode;
+    float mx[4] = {0.f, 0.f, 0.f, 0.f};
+    const int nrb = kPT / mw;  // mw <= kPT (geom_ok)
+    const int rb = tid / mw, j = tid - rb * mw;
+    if (rb < nrb) {
+      const int R2 = (mh + nrb - 1) / nrb;
+      const int i0 = rb * R2;
+      const int i1 = min(mh, i0 + R2);
+      if (i0 < i1) {
+        int cidx[L];
+#pragma unroll
+        for (int k = 0; k < L; ++k) cidx[k] = wam_ext_index(2 * j - p + k, sw, mode);
+        const int er0 = 2 * i0 - p;
+        auto hrow = [&](int t, float& lo, float& hi) {
+          const int sr = wam_ext_index(er0 + t, sh, mode);
+          float a = 0.f, d = 0.f;
+          if (sr >= 0) {
+            const float* s = lsrc + sr * sw;
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+              const float x = cidx[k] >= 0 ? s[cidx[k]] : 0.f;
+              a = fmaf(flo[k], x, a);
+              d = fmaf(fhi[k], x, d);
+            }
+          }
+          lo = a;
+          hi = d;
+        };
+        float rl[L], rh[L];
+#pragma unroll
+        for (int t = 0; t < L - 2; ++t) hrow(t, rl[t], rh[t]);
+        for (int i = i0; i < i1; ++i) {
+          const int t = 2 * (i - i0) + L - 2;
+          hrow(t, rl[L - 2], rh[L - 2]);
+          hrow(t + 1, rl[L - 1], rh[L - 1]);
+          float a = 0.f, h = 0.f, v = 0.f, d = 0.f;
+#pragma unroll
+          for (int k = 0; k < L; ++k) {
+            a = fmaf(flo[k], rl[k], a);
+            h = fmaf(fhi[k], rl[k], h);
+            v = fmaf(flo[k], rh[k], v);
+            d = fmaf(fhi[k], rh[k], d);
+          }
+          const int64_t idx = (int64_t)i * mw + j;
+          if (lastlvl) bo.put(g, g.off_a, bn, idx, a, mx[3]);
+          else ldst[idx] = a;
+          bo.put(g, g.off[l][0], bn, idx, h, mx[0]);
+          bo.put(g, g.off[l][1], bn, idx, v, mx[1]);
+          bo.put(g, g.off[l][2], bn, idx, d, mx[2]);
+#pragma unroll
+          for (int k = 0; k < L - 2; ++k) {
+            rl[k] = rl[k + 2];
+            rh[k] = rh[k + 2];
+          }
+        }
+      }
+    }
+    if constexpr (MAPS) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mx[b] = wave_max(mx[b]);
+      if (lane == 0) {
+#pragma unroll
+        for (int b = 0; b < 3; ++b) atomicMax(&wg_max[g.band[l][b]], __float_as_uint(mx[b]));
+        if (lastlvl) atomicMax(&wg_max[0], __float_as_uint(mx[3]));
+      }
+    }
+    const float* t_ = lsrc;
+    lsrc = ldst;
+    ldst = const_cast<float*>(t_);
+  }
+  if constexpr (MAPS) {
+    __syncthreads();
+    if (tid < g.nbands) {
+      const unsigned int m = wg_max[tid];
+      if (m) atomicMax(reinterpret_cast<unsigned int*>(band_max) + (item / group_items) * g.nbands + tid, m);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// filters up to 8 taps (haar, db2-db4, sym2-sym4, coif1): longer filters keep the per-level kernels,
+// whose register ring of L rows x 2 columns x lo/hi does not fit the 128-VGPR budget of 16 waves/CU
+bool l_ok(int L) { return L == 2 || L == 4 || L == 6 || L == 8; }
+
+int lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap) {
+  rowlds = kPadL + 256 + 8;  // commit covers 256 samples; pads <= p + 2 <= 20 fit behind them
+  if (rowlds < kPadL + nw0 + p->pad + 4) rowlds = kPadL + nw0 + p->pad + 4;
+  rowlds = (rowlds + 3) & ~3;
+  // buffer B (the wave rows, read and written with 16-byte ds ops) must start 16-byte aligned: a
+  // misaligned b128/b64 LDS access is split by the hardware and made this kernel 3x slower
+  llcap = p->levels > 1 ? (int)((p->lout[0][0] * p->lout[0][1] + 63) & ~63) : 0;
+  int64_t bcap = (int64_t)kPW * rowlds;
+  if (p->levels > 1) {
+    const int64_t ll2 = p->lout[1][0] * p->lout[1][1];
+    if (ll2 > bcap) bcap = ll2;
+  }
+  return (int)(llcap + bcap);
+}
+
+bool geom_ok(const wam_plan* p, int nw0, int nh0) {
+  if (p->ndim != 2 || !l_ok(p->L) || p->levels < 1 || p->levels > WAM_MAX_LEVELS) return false;
+  if (nw0 % 4 || nw0 > kPlaneMaxW || nw0 < 4 || nh0 < 1) return false;
+  if (p->lout[0][1] > kPlaneMaxMW) return false;
+  for (int l = 1; l < p->levels; ++l)
+    if (p->lout[l][1] > kPT) return false;
+  int rowlds, llcap;
+  return (int64_t)lds_floats(p, nw0, rowlds, llcap) * 4 <= kPlaneLdsCap;
+}
+
+PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items_total) {
+  PlaneGeom g{};
+  g.J = p->levels;
+  g.mode = mode;
+  g.nh0 = nh0;
+  g.nw0 = nw0;
+  for (int l = 0; l < p->levels; ++l) {
+    g.mh[l] = (int)p->lout[l][0];
+    g.mw[l] = (int)p->lout[l][1];
+    for (int s = 0; s < 3; ++s) {
+      g.band[l][s] = wam_band_of(p, l, s);
+      g.off[l][s] = p->band_off[g.band[l][s]];
+    }
+  }
+  g.off_a = p->band_off[0];
+  g.nbands = p->nbands;
+  g.items_total = items_total;
+  g.maps_item = p->band_off[p->nbands];
+  lds_floats(p, nw0, g.rowlds, g.llcap);
+  return g;
+}
+
+template <int L, int CPL, bool NOISE, int MC, bool MAPS>
+int launch_plane_t(const PlaneGeom& g, int lds_bytes, int64_t n_items, const float* in, float* out, float* band_max,
+                   const float* filt, const WamNoise& nz, int64_t S, int64_t group_items, const char* name,
+                   double bytes, hipStream_t st) {
+  auto kern = k_plane_ana<L, CPL, NOISE, MC, MAPS>;
+  static std::atomic<uint64_t> attr_set{0};  // opt in to > 64 KB of dynamic LDS, once per device
+  int dev = 0;
+  WAM_HIP_CHECK(hipGetDevice(&dev));
+  const uint64_t bit = 1ull << (dev & 63);
+  if (!(attr_set.load(std::memory_order_relaxed) & bit)) {
+    WAM_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      kPlaneLdsCap));
+    attr_set.fetch_or(bit);
+  }
+  WamTimer tm(st, name, bytes);
+  hipLaunchKernelGGL(kern, dim3((unsigned)n_items), dim3(kPT), lds_bytes, st, in, out, band_max, filt, g, nz, n_items,
+                     S, group_items);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+template <bool NOISE, int MC, bool MAPS>
+int dispatch_plane(const wam_plan* p, const PlaneGeom& g, int lds_bytes, int64_t n_items, const float* in,
+                   float* out, float* band_max, const float* filt, const WamNoise& nz, int64_t S,
+                   int64_t group_items, const char* name, double bytes, hipStream_t st) {
+  const bool two = g.mw[0] > 64;
+#define WAM_PLANE_CASE(LL)                                                                                       \
+  case LL:                                                                                                       \
+    return two ? launch_plane_t<LL, 2, NOISE, MC, MAPS>(g, lds_bytes, n_items, in, out, band_max, filt, nz, S,    \
+                                                        group_items, name, bytes, st)                            \
+               : launch_plane_t<LL, 1, NOISE, MC, MAPS>(g, lds_bytes, n_items, in, out, band_max, filt, nz, S,    \
+                                                        group_items, name, bytes, st);
+  switch (p->L) {
+    WAM_PLANE_CASE(2) WAM_PLANE_CASE(4) WAM_PLANE_CASE(6) WAM_PLANE_CASE(8)
+    default: return WAM_ERR_UNSUPPORTED;
+  }
+#undef WAM_PLANE_CASE
+}
+
+}  // namespace
+
+bool dwt2_plane_supported(const wam_plan* p, bool adjoint) {
+  const int nh0 = (int)(adjoint ? p->rec_shape[0] : p->lin[0][0]);
+  const int nw0 = (int)(adjoint ? p->rec_shape[1] : p->lin[0][1]);
+  return geom_ok(p, nw0, nh0);
+}
+
+int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in, float* coeffs, bool adjoint,
+                               const WamNoise* nz, int64_t n_samples, hipStream_t st) {
+  if (((uintptr_t)in & 15) || !dwt2_plane_supported(p, adjoint)) return WAM_ERR_UNSUPPORTED;
+  const int nh0 = (int)(adjoint ? p->rec_shape[0] : p->lin[0][0]);
+  const int nw0 = (int)(adjoint ? p->rec_shape[1] : p->lin[0][1]);
+  const int mode = adjoint ? WAM_MODE_ZERO : p->mode;
+  const float* filt = p->d_filt + (adjoint ? WAM_F_ADJ_LO : WAM_F_ANA_LO) * p->L;
+  const PlaneGeom g = make_geom(p, nh0, nw0, mode, items);
+  int rowlds, llcap;
+  const int lds_bytes = lds_floats(p, nw0, rowlds, llcap) * 4;
+  const double in_planes = nz ? (double)nz->images * nz->channels : (double)items;
+  const double bytes = 4.0 * (in_planes * nh0 * nw0 + (double)items * p->band_off[p->nbands]);
+  if (nz) {
+    if (items != n_samples * nz->images * nz->channels) return WAM_ERR_INVALID_ARG;
+    return dispatch_plane<true, 0, false>(p, g, lds_bytes, items, in, coeffs, nullptr, filt, *nz, n_samples, 1,
+                                          "k_plane_ana<noise>", bytes, st);
+  }
+  const WamNoise none{nullptr, 1, 1, 0, 0, 0};
+  return dispatch_plane<false, 0, false>(p, g, lds_bytes, items, in, coeffs, nullptr, filt, none, 1, 1,
+                                         "k_plane_ana", bytes, st);
+}
+
+int launch_dwt2_plane_maps(const wam_plan* p, int64_t images, int channels, int64_t group_items, const float* grad,
+                           float* maps, float* band_max, hipStream_t st) {
+  if (((uintptr_t)grad & 15) || !dwt2_plane_supported(p, true)) return WAM_ERR_UNSUPPORTED;
+  if (channels != 1 && channels != 3) return WAM_ERR_UNSUPPORTED;
+  const int nh0 = (int)p->rec_shape[0], nw0 = (int)p->rec_shape[1];
+  const float* filt = p->d_filt + WAM_F_ADJ_LO * p->L;
+  PlaneGeom g = make_geom(p, nh0, nw0, WAM_MODE_ZERO, images);
+  int rowlds, llcap;
+  const int lds_bytes = lds_floats(p, nw0, rowlds, llcap) * 4;
+  const WamNoise none{nullptr, 1, 1, 0, 0, 0};
+  const double bytes = 4.0 * (double)images * ((double)channels * nh0 * nw0 + (double)p->band_off[p->nbands]);
+  if (channels == 3)
+    return dispatch_plane<false, 3, true>(p, g, lds_bytes, images, grad, maps, band_max, filt, none, 1, group_items,
+                                          "k_plane_maps", bytes, st);
+  return dispatch_plane<false, 1, true>(p, g, lds_bytes, images, grad, maps, band_max, filt, none, 1, group_items,
+                                        "k_plane_maps", bytes, st);
+}

@@ -24,134 +24,11 @@
 // Waves are independent (no workgroup barriers). LDS writes and reads of a wave-private row are
 // ordered by the wave's in-order LDS queue; __builtin_amdgcn_wave_barrier() keeps the compiler
 // from reordering them.
-#include "kernels.hpp"
-#include "rng.hpp"
+#include "rowtools.hpp"
 
 namespace {
 
-constexpr int kMaxRow = 512;
-constexpr int kPadL = 24;              // >= p = L - 2 for L <= 20, multiple of 4 (16-byte commits)
-constexpr int kRowLds = kPadL + kMaxRow + 32;
-constexpr int kWaves = 4;
-
-__device__ __forceinline__ void wsync() { __builtin_amdgcn_wave_barrier(); }
-
-__device__ __forceinline__ float nan_max(float a, float b) { return (a != a || a > b) ? a : b; }
-
-__device__ __attribute__((noinline)) int ext_slow(int i, int n, int mode) { return wam_ext_index(i, n, mode); }
-
-// source row of extended row er (-1 = zero row), fast path for the interior
-__device__ __forceinline__ int row_src(int er, int n, int mode) {
-  return (er >= 0 && er < n) ? er : ext_slow(er, n, mode);
-}
-
-// One source row in registers: VEC-wide loads, MAXV per lane.
-template <int VEC, int MAXV>
-struct RowRegs {
-  float v[VEC * MAXV];
-  bool ok[MAXV];
-
-  // branch-free: out-of-range lanes / rows load a clamped valid address; the zeroing select is
-  // deferred to commit() so the load stays in flight until the row is consumed
-  __device__ __forceinline__ void fetch(const float* __restrict__ row, int nw, int lane, bool valid) {
-#pragma unroll
-    for (int q = 0; q < MAXV; ++q) {
-      const int idx = (lane + 64 * q) * VEC;
-      ok[q] = valid && idx < nw;
-      const int ci = idx < nw ? idx : nw - VEC;
-      if constexpr (VEC == 4) {
-        float4 t = *reinterpret_cast<const float4*>(row + ci);
-        v[4 * q] = t.x;
-        v[4 * q + 1] = t.y;
-        v[4 * q + 2] = t.z;
-        v[4 * q + 3] = t.w;
-      } else {
-        v[q] = row[ci];
-      }
-    }
-  }
-
-  // commit to the padded LDS row (sample s at lds[kPadL + s]); noise (optional) added here
-  __device__ __forceinline__ void commit(float* lds, int lane, const float* nz, float sg = 0.f) const {
-#pragma unroll
-    for (int q = 0; q < MAXV; ++q) {
-      const int idx = (lane + 64 * q) * VEC;
-      if constexpr (VEC == 4) {
-        float4 o = ok[q] ? make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3])
-                         : make_float4(0.f, 0.f, 0.f, 0.f);
-        if (nz) {
-          // noisy = fma(sigma, z, x): the same rounding as wam_noise_add
-          o.x = fmaf(sg, nz[4 * q], o.x);
-          o.y = fmaf(sg, nz[4 * q + 1], o.y);
-          o.z = fmaf(sg, nz[4 * q + 2], o.z);
-          o.w = fmaf(sg, nz[4 * q + 3], o.w);
-        }
-        *reinterpret_cast<float4*>(lds + kPadL + idx) = o;
-      } else {
-        lds[kPadL + idx] = ok[q] ? v[q] : 0.f;
-      }
-    }
-  }
-};
-
-// SmoothGrad noise for one fetched row (group g = e / 4 with e = (c*nh + sr)*nw + idx)
-template <int MAXV>
-__device__ __forceinline__ void make_noise(float (&nz)[4 * MAXV], int nw, int lane, int64_t row_elem0, float sg,
-                                           int64_t img, int64_t smp, uint32_t k0, uint32_t k1, bool valid) {
-#pragma unroll
-  for (int q = 0; q < MAXV; ++q) {
-    const int idx = (lane + 64 * q) * 4;
-    float z[4];
-    wam_normal4((row_elem0 + (idx < nw ? idx : 0)) >> 2, img, smp, k0, k1, z);
-    const bool ok = valid && idx < nw;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) nz[4 * q + u] = ok ? z[u] : 0.f;
-  }
-}
-
-// pad-slot refresh: lane t < npad owns ext column ext_col (left pads t - p, right pads nw + ...)
-struct PadLane {
-  int dst;   // lds index of the pad slot (or -1: this lane owns none)
-  int src;   // lds index of its source sample (or -1: zero)
-};
-
-__device__ __forceinline__ PadLane pad_lane(int lane, int nw, int p, int mode) {
-  const int npad_r = p + (nw & 1) + 1;  // right pads (one spare)
-  PadLane pl{-1, -1};
-  int e;
-  if (lane < p) e = lane - p;
-  else if (lane < p + npad_r) e = nw + (lane - p);
-  else return pl;
-  pl.dst = kPadL + e;
-  const int s = wam_ext_index(e, nw, mode);
-  pl.src = s >= 0 ? kPadL + s : -1;
-  return pl;
-}
-
-__device__ __forceinline__ void refresh_pads(float* lds, const PadLane& pl) {
-  float v = 0.f;
-  if (pl.src >= 0) v = lds[pl.src];
-  wsync();
-  if (pl.dst >= 0) lds[pl.dst] = v;
-}
-
-// Horizontal analysis of output column j from the padded LDS row (ext column 2j - p + k).
-template <int L>
-__device__ __forceinline__ void hfilter(const float* lds, int j, int p, const float (&flo)[L], const float (&fhi)[L],
-                                        float& lo, float& hi) {
-  const float2* s2 = reinterpret_cast<const float2*>(lds + kPadL + 2 * j - p);  // even offset (p even)
-  float a = 0.f, d = 0.f;
-#pragma unroll
-  for (int k = 0; k < L; k += 2) {
-    const float2 v = s2[k >> 1];
-    a = fmaf(flo[k], v.x, a);
-    d = fmaf(fhi[k], v.x, d);
-    a = fmaf(flo[k + 1], v.y, a);
-    d = fmaf(fhi[k + 1], v.y, d);
-  }
-  lo = a;
-  hi = d;
-}
+using namespace wam_rows;
 
 // ------------------------------------------------------------------------------------------------
 template <int L, int CPL, int VEC, int MAXV, bool NOISE>

@@ -334,6 +334,11 @@ bool use_rows(const wam_plan* p, int level, bool adjoint) {
   return p->ndim == 2 && !(p->flags & (WAM_PLAN_GENERIC | WAM_PLAN_NO_ROWS)) && dwt2_rows_supported(p, level, adjoint);
 }
 
+bool use_plane(const wam_plan* p, bool adjoint) {
+  return p->ndim == 2 && !(p->flags & (WAM_PLAN_GENERIC | WAM_PLAN_NO_ROWS | WAM_PLAN_NO_PLANE)) &&
+         dwt2_plane_supported(p, adjoint);
+}
+
 bool use_colstrip(const wam_plan* p) {
   return p->ndim == 2 && !(p->flags & WAM_PLAN_GENERIC) && dwt2_fused_supported(p);
 }
@@ -341,7 +346,11 @@ bool use_colstrip(const wam_plan* p) {
 // noise (level 0 only): fused SmoothGrad noise on the load; `batch` then counts the virtual
 // (sample, image, channel) planes and x holds the clean (image, channel) planes.
 int analysis_driver(const wam_plan* p, int64_t batch, const float* x, float* coeffs, void* ws, hipStream_t st,
-                    bool adjoint, const WamNoise* noise = nullptr) {
+                    bool adjoint, const WamNoise* noise = nullptr, int64_t n_samples = 1) {
+  if (use_plane(p, adjoint)) {  // all levels in one launch, LL pyramid in LDS
+    int rc = launch_dwt2_plane_analysis(p, batch, x, coeffs, adjoint, noise, n_samples, st);
+    if (rc != WAM_ERR_UNSUPPORTED) return rc;
+  }
   int nd = p->ndim;
   float* w = (float*)ws;
   int64_t ll = batch * wam_prod(p->lout[0], nd);
@@ -395,8 +404,8 @@ int wam_plan_caps(const wam_plan* p) {
   int caps = 0;
   bool rows_all = true;
   for (int l = 0; l < p->levels; ++l) rows_all = rows_all && use_rows(p, l, true);
-  if (rows_all) caps |= WAM_CAP_ADJOINT_MAPS;
-  if (use_rows(p, 0, false) && p->lin[0][1] % 4 == 0) caps |= WAM_CAP_NOISY_WAVEDEC;
+  if (rows_all || use_plane(p, true)) caps |= WAM_CAP_ADJOINT_MAPS;
+  if (use_plane(p, false) || (use_rows(p, 0, false) && p->lin[0][1] % 4 == 0)) caps |= WAM_CAP_NOISY_WAVEDEC;
   return caps;
 }
 
@@ -407,7 +416,7 @@ int wam_wavedec_noisy(const wam_plan* p, int64_t n_samples, int64_t images, int 
   const int64_t batch = n_samples * images * channels;
   if (batch == 0) return WAM_OK;
   WamNoise nz{sigma, images, channels, (uint32_t)seed, (uint32_t)(seed >> 32), sample_base};
-  return analysis_driver(p, batch, x, coeffs, ws, (hipStream_t)stream, false, &nz);
+  return analysis_driver(p, batch, x, coeffs, ws, (hipStream_t)stream, false, &nz, n_samples);
 }
 
 int wam_waverec_adjoint_maps(const wam_plan* p, int64_t groups, int64_t group_items, int channels, const float* grad,
@@ -419,6 +428,14 @@ int wam_waverec_adjoint_maps(const wam_plan* p, int64_t groups, int64_t group_it
   if (images == 0) return WAM_OK;
   hipStream_t st = (hipStream_t)stream;
   const int64_t planes = images * channels;
+  if (use_plane(p, true)) {
+    // maps from the channel-mean gradient (one pass); per-channel grads only when asked for
+    int rc = launch_dwt2_plane_maps(p, images, channels, group_items, grad, maps, band_max, st);
+    if (rc != WAM_ERR_UNSUPPORTED) {
+      if (rc || !coeff_grads) return rc;
+      return analysis_driver(p, planes, grad, coeff_grads, ws, st, true);
+    }
+  }
   float* w = (float*)ws;
   int64_t ll = planes * wam_prod(p->lout[0], 2);
   float* llbuf[2] = {w, w + ll};

@@ -147,6 +147,14 @@ def chunks(start, stop, size):
     return out
 
 
+def wam_group(model_group, total, bytes_per_sample, budget_bytes=8 << 30):
+    """Samples (IG steps) per WAM transform launch: a multiple of the model group, as many as the
+    rank's range and a device-memory budget allow. The transforms then run on thousands of planes
+    per launch (full-chip grids, one launch per pass) while the model still sees `model_group`."""
+    k = max(1, int(budget_bytes // max(1, bytes_per_sample)) // max(1, model_group))
+    return max(1, min(total, k * model_group))
+
+
 def auto_group(model, n_items, requested, cap_items=256):
     if requested is not None:
         return max(1, int(requested))

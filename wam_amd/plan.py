@@ -169,6 +169,7 @@ def get_plan(ndim, shape, levels, wavelet, mode, device, generic=False, flags=No
 
 
 PLAN_NO_ROWS = 2
+PLAN_NO_PLANE = 4
 CAP_NOISY_WAVEDEC = 1
 CAP_ADJOINT_MAPS = 2
 

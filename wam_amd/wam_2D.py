@@ -25,7 +25,7 @@ import torch.nn.functional as F
 from . import frames
 from .constants import WaveletDetailTuple2d
 from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, legacy_noise, model_device,
-                     require_gpu_device)
+                     require_gpu_device, wam_group)
 from .plan import (CAP_ADJOINT_MAPS, CAP_NOISY_WAVEDEC, frame_accumulate, frame_trapz, get_plan, item_sigma,
                    noise_add, reproject_scales, subband_maps)
 
@@ -119,10 +119,14 @@ class BaseWAM2D:
 
     # ------------------------------------------------------------------ lazy side attributes
     def _record_pass(self, plan, coeff_flat, grad_flat, batch_items, first_item, n, c, coeff_items=None,
-                     coeff_first=None):
+                     coeff_first=None, grad_img=None):
+        """Keep the last gradient pass (the reference's self.wavelet_coeffs / gradient_coeffs /
+        scales, lib/wam_2D.py:120-128) on the device; host copies are made on first access.
+        grad_img (optional): the input gradient [n*c, *rec] of that pass -- its coefficient
+        gradients are then computed on access instead of in the hot loop."""
         ci = batch_items if coeff_items is None else coeff_items
         cf = first_item if coeff_first is None else coeff_first
-        self._pass = (plan, (coeff_flat, ci, cf), (grad_flat, batch_items, first_item), n, c)
+        self._pass = (plan, (coeff_flat, ci, cf), (grad_flat, batch_items, first_item), n, c, grad_img)
         self._wavelet_coeffs = None
         self._gradient_coeffs = None
         self._scales = None
@@ -130,7 +134,7 @@ class BaseWAM2D:
     @property
     def wavelet_coeffs(self):
         if self._wavelet_coeffs is None and self._pass is not None:
-            plan, (cf, b, f), _, n, c = self._pass
+            plan, (cf, b, f), _, n, c, _ = self._pass
             self._wavelet_coeffs = _to_numpy_2d(plan, cf, b, n, c, f)
         return self._wavelet_coeffs
 
@@ -141,7 +145,9 @@ class BaseWAM2D:
     @property
     def gradient_coeffs(self):
         if self._gradient_coeffs is None and self._pass is not None:
-            plan, _, (gf, b, f), n, c = self._pass
+            plan, _, (gf, b, f), n, c, gimg = self._pass
+            if gimg is not None:
+                gf, b, f = plan.adjoint(gimg), n * c, 0
             self._gradient_coeffs = _to_numpy_2d(plan, gf, b, n, c, f)
         return self._gradient_coeffs
 
@@ -296,6 +302,20 @@ class WaveletAttribution2D(BaseWAM2D):
         self._scales = None
 
     # ------------------------------------------------------------------ estimators
+    def _wam_group(self, plan, n, c, model_group, total):
+        per_sample = 4 * n * (c * plan.coeff_numel + 2 * c * int(np.prod(plan.rec_shape)) + plan.coeff_numel)
+        return wam_group(model_group, total, per_sample)
+
+    def _gradients(self, imgs, y, groups, n, model_group):
+        """Input gradients of `groups` stacked reference calls, model run `model_group` at a time."""
+        if groups <= model_group:
+            return input_gradient(self.model, imgs, y, groups, n, self.autocast_dtype, self.channels_last)
+        out = torch.empty_like(imgs)
+        for s0, cnt in chunks(0, groups, model_group):
+            out[s0 * n:(s0 + cnt) * n] = input_gradient(self.model, imgs[s0 * n:(s0 + cnt) * n], y, cnt, n,
+                                                        self.autocast_dtype, self.channels_last)
+        return out
+
     def smooth_gradcam(self, x, y):
         """lib/wam_2D.py:379-415."""
         dev = self._dev
@@ -308,6 +328,8 @@ class WaveletAttribution2D(BaseWAM2D):
         shard = Shard(self.dist)
         s_lo, s_hi = shard.range(self.n_samples)
         group = auto_group(self.model, n, self.sample_batch)
+        # parity mode streams the host-generated legacy noise one model group at a time
+        wgroup = group if self.noise == "numpy" else self._wam_group(plan, n, c, group, s_hi - s_lo)
         frame = torch.zeros(n * rh * rw, dtype=torch.float64, device=dev)
         noise_it = None
         if self.noise == "numpy":
@@ -315,9 +337,7 @@ class WaveletAttribution2D(BaseWAM2D):
                                     list(range(s_lo, s_hi)))
         rec = plan.rec_shape
         last = None
-        work = chunks(s_lo, s_hi, group)
-        for ci, (s0, cnt) in enumerate(work):
-            is_last = ci == len(work) - 1
+        for s0, cnt in chunks(s_lo, s_hi, wgroup):
             if noise_it is not None:
                 arr = np.stack([next(noise_it)[1] for _ in range(cnt)])
                 host = torch.from_numpy(arr).pin_memory().to(dev, non_blocking=True)
@@ -329,13 +349,13 @@ class WaveletAttribution2D(BaseWAM2D):
                 noisy = noise_add(x, sigma, cnt, n, item, item, seed=self.random_seed, sample_base=s0)
                 flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
             img = plan.waverec(flat, cnt * n * c)[0].view((cnt * n, c) + rec)
-            g = input_gradient(self.model, img, y, cnt, n, self.autocast_dtype, self.channels_last)
-            maps, bmax, cg = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=is_last)
+            g = self._gradients(img, y, cnt, n, group)
+            maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
             frame_accumulate(cnt, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, frame)
-            if is_last:
-                last = (plan, flat, cg, cnt * n * c, (cnt - 1) * n, n, c)
+            last = (plan, flat, None, cnt * n * c, (cnt - 1) * n, n, c)
+            last_g = g[(cnt - 1) * n:].reshape((n * c,) + rec)
         if last is not None:
-            self.wam._record_pass(*last)
+            self.wam._record_pass(*last, grad_img=last_g)
         shard.all_reduce_sum(frame)
         avg = frame.view(n, rh, rw) / self.n_samples
         self._set_result(avg)
@@ -356,26 +376,26 @@ class WaveletAttribution2D(BaseWAM2D):
         shard = Shard(self.dist)
         k_lo, k_hi = shard.range(self.n_samples)
         group = auto_group(self.model, n, self.sample_batch)
+        wgroup = self._wam_group(plan, n, c, group, k_hi - k_lo)
         acc = torch.zeros(n * rh * rw, dtype=torch.float32, device=dev)
         prev = torch.zeros_like(acc)
         rec = plan.rec_shape
         last = None
-        work = chunks(k_lo, k_hi, group)
-        for ci, (k0, cnt) in enumerate(work):
+        for k0, cnt in chunks(k_lo, k_hi, wgroup):
             img = plan.waverec(z, n * c, alphas=alphas[k0:k0 + cnt]).view((cnt * n, c) + rec)
-            g = input_gradient(self.model, img, y, cnt, n, self.autocast_dtype, self.channels_last)
-            maps, bmax, cg = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c,
-                                                full=ci == len(work) - 1)
+            g = self._gradients(img, y, cnt, n, group)
+            maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
             weights = None
             if shard.world > 1:
                 weights = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
             frame_trapz(cnt, k0, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, prev, acc,
                         weights)
-            last = (plan, None, cg, cnt * n * c, (cnt - 1) * n, n, c, float(alphas[k0 + cnt - 1]))
+            last = (plan, float(alphas[k0 + cnt - 1]))
+            last_g = g[(cnt - 1) * n:].reshape((n * c,) + rec)
         if last is not None:
-            plan_, _, cg, b, f, nn, cc, alpha = last
+            plan_, alpha = last
             coeff = z * float(np.float32(alpha))  # the path coefficients alpha * z of the last step
-            self.wam._record_pass(plan_, coeff, cg, b, f, nn, cc, coeff_items=n * c, coeff_first=0)
+            self.wam._record_pass(plan_, coeff, None, n * c, 0, n, c, grad_img=last_g)
         shard.all_reduce_sum(acc)
         out = base.view(n, rh, rw) * acc.view(n, rh, rw).double()
         self._set_result(out)
