@@ -263,6 +263,13 @@ def test_plane_resident_equals_per_level(wam, wav, shape, J, mode):
     g = torch.randn((B,) + fast.rec_shape, device="cuda")
     a, c = fast.adjoint(g), gen.adjoint(g)
     assert float((a - c).abs().max()) < 1e-5
+    cf = gen.wavedec(x)
+    a, b, c = fast.waverec(cf, B), ref.waverec(cf, B), gen.waverec(cf, B)
+    assert torch.equal(a, b)  # same arithmetic order as the per-level synthesis kernel
+    assert float((a - c).abs().max()) < 1e-5
+    al = [0.0, 0.25, 1.0 / 3.0, 1.0]
+    a, b = fast.waverec(cf, B, alphas=al), ref.waverec(cf, B, alphas=al)
+    assert a.shape == (len(al), B) + fast.rec_shape and torch.equal(a, b)
     N, C = 5, 3
     xs = torch.randn((N, C) + shape, device="cuda")
     sigma = wam.item_sigma(xs, C * shape[0] * shape[1], C * shape[0] * shape[1], 0.25)

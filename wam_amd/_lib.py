@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libwam_hip.so")
+LIB_PATH = os.environ.get("WAM_LIB_PATH") or os.path.join(_HERE, "libwam_hip.so")  # override: experiments
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "wam_hip.h")
 
 if not os.path.exists(LIB_PATH):

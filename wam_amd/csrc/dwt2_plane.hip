@@ -23,6 +23,8 @@
 // Workgroup order: an XCD-aware bijective swizzle makes consecutive logical workgroups share an
 // XCD (L2); for noisy analysis the logical order is sample-fastest, so the S noise samples of one
 // clean plane run back to back on one XCD and its rows are read from HBM about once.
+#include <stdlib.h>
+
 #include <atomic>
 
 #include "rowtools.hpp"
@@ -50,6 +52,7 @@ struct PlaneGeom {
   int64_t maps_item;                // packed floats per item (maps mode)
   int rowlds;                       // floats per wave-private row
   int llcap;                        // floats of LDS buffer A (LL_1, LL_3, ...)
+  int sample_fast;                  // noisy analysis: logical order sample-fastest (1) or plane-fastest (0)
 };
 
 template <bool MAPS>
@@ -104,9 +107,15 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
   float sg = 0.f;
   if constexpr (NOISE) {
     const int64_t nc = nz.images * nz.channels;
-    src_plane = lwg / S;                  // sample-fastest: the S samples of a plane are adjacent
-    const int64_t s = lwg % S;
-    item = s * nc + src_plane;            // output planes are (sample, image, channel)
+    int64_t s;
+    if (g.sample_fast) {
+      src_plane = lwg / S;                // sample-fastest: the S samples of a plane are adjacent
+      s = lwg % S;
+      item = s * nc + src_plane;          // output planes are (sample, image, channel)
+    } else {
+      s = lwg / nc;
+      src_plane = lwg % nc;
+    }
     smp = nz.sample_base + s;
     img = src_plane / nz.channels;
     ch = src_plane % nz.channels;
@@ -355,6 +364,205 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
   }
 }
 
+// ================================================================================================
+// Plane-resident multi-level synthesis (waverec2 with the IG alpha fused): one workgroup per
+// (plane, alpha); the reconstructed approximations LL'_J-1 .. LL'_1 stay in LDS, every level is a
+// streaming pass of the waves over coefficient rows (the per-lane vertical ring / LDS exchange
+// scheme of k_dwt2_syn, same arithmetic order), coefficient rows are prefetched kSynPF rows ahead
+// with clamped, unconditional loads; only level 0 writes to HBM.
+constexpr int kMaxAlpha = 128;
+constexpr int kSynPF = 4;
+
+struct SynGeom {
+  int J;
+  int mh[WAM_MAX_LEVELS], mw[WAM_MAX_LEVELS];  // coefficient dims of level l (0 = finest)
+  int oh[WAM_MAX_LEVELS], ow[WAM_MAX_LEVELS];  // output dims of level l (l >= 1: LL'_l = lout[l-1])
+  int64_t off_a;
+  int64_t off[WAM_MAX_LEVELS][3];
+  int64_t batch;     // items in the band-major coefficient buffer
+  int lcap, scap;    // floats of LDS buffers L (odd levels' outputs) and S (even levels' outputs)
+  int n_alpha;       // alphas in this launch
+  int64_t out_base;  // output item offset of alpha 0 of this launch
+};
+
+struct SynAlphas {
+  float v[kMaxAlpha];
+};
+
+// one level's streaming synthesis for (strip, coefficient rows [qbeg, qend)) of one wave
+template <int L>
+__device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float sa, const float* __restrict__ pH,
+                                           const float* __restrict__ pV, const float* __restrict__ pD, float sd,
+                                           int mh, int mw, float* __restrict__ dst, int oh, int ow, int strip,
+                                           int qbeg, int qend, float4* xch, const float (&rlo)[L],
+                                           const float (&rhi)[L], int lane) {
+  constexpr int p = L - 2;
+  constexpr int H2 = L / 2;
+  constexpr int OUTQ = 65 - H2;
+  constexpr int PF = kSynPF;
+  const int qs = p >> 1;
+  const int jj = qs + strip * OUTQ - (H2 - 1) + lane;
+  const bool colv = jj >= 0 && jj < mw;
+  const int jc = min(max(jj, 0), mw - 1);
+  const bool producer = lane >= H2 - 1;
+  const int ucol = 2 * (jj - qs);
+  // raw fetched rows (a, h, v, d) + validity; scaled / zeroed when they enter the ring
+  float fa[PF], fh[PF], fv[PF], fd[PF];
+  bool fok[PF];
+  auto fetch = [&](int u, int q) {
+    fok[u] = colv && q >= 0 && q < mh;
+    const int o = min(max(q, 0), mh - 1) * mw + jc;
+    fa[u] = pA[o];
+    fh[u] = pH[o];
+    fv[u] = pV[o];
+    fd[u] = pD[o];
+  };
+  float ra[H2], rh[H2], rv[H2], rd[H2];
+#pragma unroll
+  for (int k = 0; k < H2 - 1; ++k) {
+    fetch(0, qbeg - (H2 - 1) + k);
+    ra[k] = fok[0] ? sa * fa[0] : 0.f;
+    rh[k] = fok[0] ? sd * fh[0] : 0.f;
+    rv[k] = fok[0] ? sd * fv[0] : 0.f;
+    rd[k] = fok[0] ? sd * fd[0] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < PF; ++u) fetch(u, qbeg + u);
+  for (int base = qbeg; base < qend; base += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int q = base + u;
+      ra[H2 - 1] = fok[u] ? sa * fa[u] : 0.f;
+      rh[H2 - 1] = fok[u] ? sd * fh[u] : 0.f;
+      rv[H2 - 1] = fok[u] ? sd * fv[u] : 0.f;
+      rd[H2 - 1] = fok[u] ? sd * fd[u] : 0.f;
+      fetch(u, q + PF);  // past the chunk: clamped, never used
+      float lo0 = 0.f, lo1 = 0.f, hi0 = 0.f, hi1 = 0.f;
+#pragma unroll
+      for (int i2 = 0; i2 < H2; ++i2) {
+        const int sl = H2 - 1 - i2;
+        lo0 = fmaf(rlo[2 * i2], ra[sl], lo0);
+        lo0 = fmaf(rhi[2 * i2], rh[sl], lo0);
+        lo1 = fmaf(rlo[2 * i2 + 1], ra[sl], lo1);
+        lo1 = fmaf(rhi[2 * i2 + 1], rh[sl], lo1);
+        hi0 = fmaf(rlo[2 * i2], rv[sl], hi0);
+        hi0 = fmaf(rhi[2 * i2], rd[sl], hi0);
+        hi1 = fmaf(rlo[2 * i2 + 1], rv[sl], hi1);
+        hi1 = fmaf(rhi[2 * i2 + 1], rd[sl], hi1);
+      }
+      xch[lane] = make_float4(lo0, lo1, hi0, hi1);
+      wsync();
+      if (producer && q < qend) {
+        float o00 = 0.f, o01 = 0.f, o10 = 0.f, o11 = 0.f;
+#pragma unroll
+        for (int i2 = 0; i2 < H2; ++i2) {
+          const float4 n = xch[lane - i2];
+          o00 = fmaf(rlo[2 * i2], n.x, o00);
+          o00 = fmaf(rhi[2 * i2], n.z, o00);
+          o01 = fmaf(rlo[2 * i2 + 1], n.x, o01);
+          o01 = fmaf(rhi[2 * i2 + 1], n.z, o01);
+          o10 = fmaf(rlo[2 * i2], n.y, o10);
+          o10 = fmaf(rhi[2 * i2], n.w, o10);
+          o11 = fmaf(rlo[2 * i2 + 1], n.y, o11);
+          o11 = fmaf(rhi[2 * i2 + 1], n.w, o11);
+        }
+        const int r0 = 2 * (q - qs);
+        if (ucol >= 0 && ucol < ow) {
+          const bool two = ucol + 1 < ow;
+          if (r0 < oh) {
+            float* d0 = dst + (int64_t)r0 * ow + ucol;
+            if (two) *reinterpret_cast<float2*>(d0) = make_float2(o00, o01);
+            else d0[0] = o00;
+          }
+          if (r0 + 1 < oh) {
+            float* d1 = dst + (int64_t)(r0 + 1) * ow + ucol;
+            if (two) *reinterpret_cast<float2*>(d1) = make_float2(o10, o11);
+            else d1[0] = o10;
+          }
+        }
+      }
+      wsync();
+#pragma unroll
+      for (int k = 0; k < H2 - 1; ++k) {
+        ra[k] = ra[k + 1];
+        rh[k] = rh[k + 1];
+        rv[k] = rv[k + 1];
+        rd[k] = rd[k + 1];
+      }
+    }
+  }
+}
+
+// the waves of the workgroup split a level into strips x row chunks
+template <int L>
+__device__ __forceinline__ bool syn_work(int oh, int ow, int wv, int& strip, int& qbeg, int& qend) {
+  constexpr int p = L - 2;
+  constexpr int OUTQ = 65 - L / 2;
+  const int qs = p >> 1;
+  const int nstrips = ((ow + 1) / 2 + OUTQ - 1) / OUTQ;
+  const int chunks = kPW / nstrips;
+  strip = wv % nstrips;
+  const int chunk = wv / nstrips;
+  const int qlast = (p + oh - 1) >> 1;
+  const int nq = qlast - qs + 1;
+  const int RQ = (nq + chunks - 1) / chunks;
+  qbeg = qs + chunk * RQ;
+  qend = min(qbeg + RQ, qlast + 1);
+  return chunk < chunks && qbeg < qend;
+}
+
+template <int L>
+__global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8)))
+    k_plane_syn(const float* __restrict__ coeffs, float* __restrict__ out, const float* __restrict__ filt, SynGeom g,
+                SynAlphas al, int64_t n_items) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int64_t nwg = gridDim.x, bid = blockIdx.x;
+  const int64_t q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const int64_t lwg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  if (lwg >= n_items) return;  // never taken (grid == n_items)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // alpha-fastest: the alphas of one plane share an XCD and its coefficient reads
+  const int64_t item = lwg / g.n_alpha;
+  const int ai = (int)(lwg % g.n_alpha);
+  const float s = al.v[ai];
+  float rlo[L], rhi[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    rlo[k] = filt[k];
+    rhi[k] = filt[L + k];
+  }
+  float* bufL = smem;
+  float* bufS = smem + g.lcap;
+  float4* xch = reinterpret_cast<float4*>(smem + g.lcap + g.scap) + wv * 64;
+  for (int l = g.J - 1; l >= 0; --l) {
+    if (l < g.J - 1) __syncthreads();  // LL'_{l+1} complete
+    const int mh = g.mh[l], mw = g.mw[l], oh = g.oh[l], ow = g.ow[l];
+    const int64_t bn = (int64_t)mh * mw;
+    const float* pH = coeffs + g.batch * g.off[l][0] + item * bn;
+    const float* pV = coeffs + g.batch * g.off[l][1] + item * bn;
+    const float* pD = coeffs + g.batch * g.off[l][2] + item * bn;
+    int strip, qbeg, qend;
+    if (!syn_work<L>(oh, ow, wv, strip, qbeg, qend)) continue;
+    const bool coarsest = l == g.J - 1;
+    if (l == 0) {
+      float* dst = out + (g.out_base + (int64_t)ai * g.batch + item) * ((int64_t)oh * ow);
+      if (coarsest)
+        syn_stream<L>(coeffs + g.batch * g.off_a + item * bn, s, pH, pV, pD, s, mh, mw, dst, oh, ow, strip, qbeg,
+                      qend, xch, rlo, rhi, lane);
+      else
+        syn_stream<L>(bufL, 1.f, pH, pV, pD, s, mh, mw, dst, oh, ow, strip, qbeg, qend, xch, rlo, rhi, lane);
+    } else {
+      float* dst = (l & 1) ? bufL : bufS;
+      if (coarsest)
+        syn_stream<L>(coeffs + g.batch * g.off_a + item * bn, s, pH, pV, pD, s, mh, mw, dst, oh, ow, strip, qbeg,
+                      qend, xch, rlo, rhi, lane);
+      else
+        syn_stream<L>((l & 1) ? bufS : bufL, 1.f, pH, pV, pD, s, mh, mw, dst, oh, ow, strip, qbeg, qend, xch, rlo,
+                      rhi, lane);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // filters up to 8 taps (haar, db2-db4, sym2-sym4, coif1): longer filters keep the per-level kernels,
 // whose register ring of L rows x 2 columns x lo/hi does not fit the 128-VGPR budget of 16 waves/CU
@@ -404,6 +612,8 @@ PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items
   g.items_total = items_total;
   g.maps_item = p->band_off[p->nbands];
   lds_floats(p, nw0, g.rowlds, g.llcap);
+  const char* o = getenv("WAM_NOISE_ORDER");
+  g.sample_fast = !(o && o[0] == 'p');
   return g;
 }
 
@@ -492,4 +702,85 @@ int launch_dwt2_plane_maps(const wam_plan* p, int64_t images, int channels, int6
                                           "k_plane_maps", bytes, st);
   return dispatch_plane<false, 1, true>(p, g, lds_bytes, images, grad, maps, band_max, filt, none, 1, group_items,
                                         "k_plane_maps", bytes, st);
+}
+
+// ------------------------------------------------------------------------------------------------ synthesis host
+namespace {
+
+int syn_lds_floats(const wam_plan* p, int& lcap, int& scap) {
+  lcap = p->levels > 1 ? (int)((p->lout[0][0] * p->lout[0][1] + 63) & ~63) : 0;
+  scap = p->levels > 2 ? (int)((p->lout[1][0] * p->lout[1][1] + 63) & ~63) : 0;
+  return lcap + scap + kPW * 64 * 4;
+}
+
+bool syn_ok(const wam_plan* p) {
+  if (p->ndim != 2 || !l_ok(p->L) || p->levels < 1 || p->levels > WAM_MAX_LEVELS) return false;
+  const int outq = 65 - p->L / 2;
+  for (int l = 0; l < p->levels; ++l) {
+    const int64_t ow = l ? p->lout[l - 1][1] : p->rec_shape[1];
+    if (((ow + 1) / 2 + outq - 1) / outq > kPW) return false;
+  }
+  int lcap, scap;
+  return (int64_t)syn_lds_floats(p, lcap, scap) * 4 <= kPlaneLdsCap;
+}
+
+template <int L>
+int launch_syn_plane_t(const SynGeom& g, int lds_bytes, int64_t n_items, const float* coeffs, float* out,
+                       const float* filt, const SynAlphas& al, double bytes, hipStream_t st) {
+  auto kern = k_plane_syn<L>;
+  static std::atomic<uint64_t> attr_set{0};
+  int dev = 0;
+  WAM_HIP_CHECK(hipGetDevice(&dev));
+  const uint64_t bit = 1ull << (dev & 63);
+  if (!(attr_set.load(std::memory_order_relaxed) & bit)) {
+    WAM_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      kPlaneLdsCap));
+    attr_set.fetch_or(bit);
+  }
+  WamTimer tm(st, "k_plane_syn", bytes);
+  hipLaunchKernelGGL(kern, dim3((unsigned)n_items), dim3(kPT), lds_bytes, st, coeffs, out, filt, g, al, n_items);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+}  // namespace
+
+bool dwt2_plane_syn_supported(const wam_plan* p) { return syn_ok(p); }
+
+int launch_dwt2_plane_synthesis(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha,
+                                int n_alpha, float* out, hipStream_t st) {
+  if (!syn_ok(p)) return WAM_ERR_UNSUPPORTED;
+  SynGeom g{};
+  g.J = p->levels;
+  for (int l = 0; l < p->levels; ++l) {
+    g.mh[l] = (int)p->lout[l][0];
+    g.mw[l] = (int)p->lout[l][1];
+    g.oh[l] = (int)(l ? p->lout[l - 1][0] : p->rec_shape[0]);
+    g.ow[l] = (int)(l ? p->lout[l - 1][1] : p->rec_shape[1]);
+    for (int k = 0; k < 3; ++k) g.off[l][k] = p->band_off[wam_band_of(p, l, k)];
+  }
+  g.off_a = p->band_off[0];
+  g.batch = batch;
+  const int lds_bytes = syn_lds_floats(p, g.lcap, g.scap) * 4;
+  const float* filt = p->d_filt + WAM_F_SYN_LO * p->L;
+  const double out_item = (double)p->rec_shape[0] * p->rec_shape[1];
+  for (int a0 = 0; a0 < n_alpha; a0 += kMaxAlpha) {
+    const int na = n_alpha - a0 < kMaxAlpha ? n_alpha - a0 : kMaxAlpha;
+    SynAlphas al{};
+    for (int i = 0; i < na; ++i) al.v[i] = alpha ? alpha[a0 + i] : 1.0f;
+    g.n_alpha = na;
+    g.out_base = (int64_t)a0 * batch;
+    // algorithmic bytes: the coefficients once, every reconstruction once
+    const double bytes = 4.0 * ((double)batch * p->band_off[p->nbands] + (double)na * batch * out_item);
+    int rc;
+    switch (p->L) {
+      case 2: rc = launch_syn_plane_t<2>(g, lds_bytes, batch * na, coeffs, out, filt, al, bytes, st); break;
+      case 4: rc = launch_syn_plane_t<4>(g, lds_bytes, batch * na, coeffs, out, filt, al, bytes, st); break;
+      case 6: rc = launch_syn_plane_t<6>(g, lds_bytes, batch * na, coeffs, out, filt, al, bytes, st); break;
+      case 8: rc = launch_syn_plane_t<8>(g, lds_bytes, batch * na, coeffs, out, filt, al, bytes, st); break;
+      default: rc = WAM_ERR_UNSUPPORTED;
+    }
+    if (rc) return rc;
+  }
+  return WAM_OK;
 }

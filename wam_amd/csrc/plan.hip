@@ -458,6 +458,11 @@ int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const flo
   if (!alpha && n_alpha != 1) return WAM_ERR_INVALID_ARG;
   if (batch == 0) return WAM_OK;
   hipStream_t st = (hipStream_t)stream;
+  if (p->ndim == 2 && !(p->flags & (WAM_PLAN_GENERIC | WAM_PLAN_NO_ROWS | WAM_PLAN_NO_PLANE)) &&
+      dwt2_plane_syn_supported(p)) {  // all levels and all alphas in one launch
+    int rc = launch_dwt2_plane_synthesis(p, batch, coeffs, alpha, n_alpha, out, st);
+    if (rc != WAM_ERR_UNSUPPORTED) return rc;
+  }
   int nd = p->ndim;
   int64_t out_item = wam_prod(p->rec_shape, nd);
   int64_t rec_ll = 0;
