@@ -75,8 +75,9 @@ def cpu_baseline(seconds):
     wam_ref.smooth_2d(model, x[:1], y[:1], wavelet="db4", J=3, mode="reflect", n_samples=1, frame="native")
     t1 = time.perf_counter() - t0
     per = max(t1, 1e-3)
-    n_img = int(max(1, min(4, seconds / per / 4)))
-    n_s = int(max(1, min(N_SAMPLES, seconds / per / n_img)))
+    # images x samples sized to ~`seconds` of CPU work: all 25 samples of as many images as fit
+    n_s = N_SAMPLES if seconds / per >= N_SAMPLES else int(max(1, seconds / per))
+    n_img = int(max(1, min(N_IMAGES, seconds / per / n_s)))
     t0 = time.perf_counter()
     wam_ref.smooth_2d(model, x[:n_img], y[:n_img], wavelet="db4", J=3, mode="reflect", n_samples=n_s, frame="native")
     dt = time.perf_counter() - t0

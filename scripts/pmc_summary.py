@@ -19,8 +19,13 @@ def short(name):
     if not m:
         return None
     base = m.group(1)
-    if base == "k_ana_rows" and m.group(3) and m.group(3).split(",")[-1].strip() == "true":
+    args = [a.strip() for a in m.group(3).split(",")] if m.group(3) else []
+    if base == "k_ana_rows" and args and args[-1] == "true":
         return "k_ana_rows<noise>"
+    if base == "k_plane_ana" and len(args) >= 5:  # <L, CPL, NOISE, MC, MAPS>
+        if args[4] == "true":
+            return "k_plane_maps"
+        return "k_plane_ana<noise>" if args[2] == "true" else "k_plane_ana"
     return base
 
 

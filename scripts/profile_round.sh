@@ -23,7 +23,7 @@ step() {  # step <seconds> <name> <cmd...>
 step 150 kbench python3 $R/scripts/kbench.py --iters 20 &&
 step 300 trace rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench -- \
   python3 $R/bench.py --steps 3 --warmup 1 --cpu-baseline off "$@" &&
-step 240 pmc_fetch rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'wam_k|k_(ana|adj|dwt|frame|item|noise|cube|subband|acc|trapz|reproj|syn)' --output-format csv -d $O/pmc_fetch -o bench -- \
+step 240 pmc_fetch rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'k_(plane|ana|adj|dwt|frame|item|noise|cube|subband|acc|trapz|reproj|syn)' --output-format csv -d $O/pmc_fetch -o bench -- \
   python3 $R/bench.py --steps 1 --warmup 1 --cpu-baseline off "$@" &&
-step 240 pmc_write rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'wam_k|k_(ana|adj|dwt|frame|item|noise|cube|subband|acc|trapz|reproj|syn)' --output-format csv -d $O/pmc_write -o bench -- \
+step 240 pmc_write rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'k_(plane|ana|adj|dwt|frame|item|noise|cube|subband|acc|trapz|reproj|syn)' --output-format csv -d $O/pmc_write -o bench -- \
   python3 $R/bench.py --steps 1 --warmup 1 --cpu-baseline off "$@"
