@@ -102,11 +102,17 @@ def frame_geometry(frame, H, W, h1w, reproject=False):
 
 
 def smooth_2d(model, x, y, wavelet="haar", J=3, mode="reflect", n_samples=25, stdev_spread=0.25,
-              random_seed=42, normalize=True, frame="legacy", keep_last=None):
+              random_seed=42, normalize=True, frame="legacy", keep_last=None, noise=None):
+    """noise (test hook): float32 [n_samples, N, C, H, W] added instead of the legacy numpy stream
+    (used to check the GPU's Philox perf mode with the same glue)."""
     H, W = x.shape[2], x.shape[3]
     avg = np.zeros((x.shape[0], H, W))
     last = None
-    for _, noisy in legacy_noise_stream(x, n_samples, stdev_spread, random_seed):
+    if noise is not None:
+        stream = ((s, x + torch.from_numpy(np.ascontiguousarray(noise[s]))) for s in range(n_samples))
+    else:
+        stream = legacy_noise_stream(x, n_samples, stdev_spread, random_seed)
+    for _, noisy in stream:
         c, g = single_pass_2d(model, noisy, y, wavelet, J, mode)
         canvas, base = frame_geometry(frame, H, W, g[-1][0].shape[-1])
         avg += mosaic_2d(g, normalize, canvas, base)

@@ -202,3 +202,39 @@ def test_sample_batching_invariance(W):
         ex = W.WaveletAttribution2D(testmodels.TinySmooth2D().cuda(), wavelet="haar", n_samples=5, sample_batch=sb)
         outs.append(ex(x, [0, 1, 2]))
     assert np.abs(outs[0] - outs[1]).max() < 1e-5 and np.abs(outs[0] - outs[2]).max() < 1e-5
+
+
+def test_philox_fused_path_matches_oracle(W):
+    """The bench's perf path (Philox noise fused into the plane-resident analysis, native frame,
+    db4, several model chunks in one WAM group) vs the reference glue fed the same noise values."""
+    from oracle import wam_ref
+    from wam_amd import plan as P
+    rs = np.random.RandomState(21)
+    N, C, H = 2, 3, 224
+    S = 5
+    x = torch.tensor(rs.standard_normal((N, C, H, H)).astype(np.float32))
+    y = [3, 7]
+    xd = x.cuda()
+    item = C * H * H
+    sigma = P.item_sigma(xd, item, item, 0.25)
+    noise = P.noise_add(torch.zeros_like(xd), sigma, S, N, item, item, seed=42, sample_base=0)
+    noise = noise.view(S, N, C, H, H).cpu().numpy()
+    ref = wam_ref.smooth_2d(testmodels.TinySmooth2D(), x, y, wavelet="db4", J=3, n_samples=S, frame="native",
+                            noise=noise)
+    ex = W.WaveletAttribution2D(testmodels.TinySmooth2D().cuda(), wavelet="db4", J=3, n_samples=S,
+                                noise="philox", frame="native", sample_batch=2)
+    out = ex(x, y)
+    assert out.shape == ref.shape
+    assert np.abs(out - ref).max() < 1e-4, np.abs(out - ref).max()
+
+
+def test_wam_group_size_invariance(W, monkeypatch):
+    """Transform launches over the whole sample range vs one model group at a time: same map."""
+    import wam_amd.wam_2D as m2
+    rs = np.random.RandomState(22)
+    x = torch.tensor(rs.standard_normal((3, 3, 224, 224)).astype(np.float32))
+    kw = dict(wavelet="db4", J=3, n_samples=7, noise="philox", frame="native", sample_batch=2)
+    full = W.WaveletAttribution2D(testmodels.TinySmooth2D().cuda(), **kw)(x, [0, 1, 2])
+    monkeypatch.setattr(m2, "wam_group", lambda model_group, total, per_sample: model_group)
+    small = W.WaveletAttribution2D(testmodels.TinySmooth2D().cuda(), **kw)(x, [0, 1, 2])
+    assert np.abs(full - small).max() < 1e-6
