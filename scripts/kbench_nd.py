@@ -1,0 +1,39 @@
+"""Per-launch timing of the 1D (c3) and 3D (c5) transforms at the BASELINE config shapes.
+
+usage: python scripts/kbench_nd.py [--iters 5]
+c3: 1D db6 J=5, 256 clips x 80000 samples x 25 noise samples per launch group (6400 signals)
+c5: 3D haar J=2 symmetric, 16 volumes of 128^3 x 25 samples (400 volumes)
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import wam_amd  # noqa: E402,F401
+from scripts.kbench import run  # noqa: E402
+from wam_amd import plan as P  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=5)
+    args = ap.parse_args()
+    torch.manual_seed(0)
+    for tag, dim, shape, J, wav, mode, B in [("c3 1D", 1, (80000,), 5, "db6", "reflect", 6400),
+                                             ("c5 3D", 3, (128, 128, 128), 2, "haar", "symmetric", 400)]:
+        p = P.get_plan(dim, shape, J, wav, mode, "cuda")
+        x = torch.randn((B,) + shape, device="cuda")
+        run(f"{tag} wavedec B={B}", lambda: p.wavedec(x), args.iters)
+        cf = p.wavedec(x)
+        run(f"{tag} waverec", lambda: p.waverec(cf, B), args.iters)
+        del cf
+        g = torch.randn((B,) + p.rec_shape, device="cuda")
+        run(f"{tag} adjoint", lambda: p.adjoint(g), args.iters)
+        del g, x
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -296,3 +296,45 @@ def test_plane_maps_band_max_over_many_groups(wam):
     gi = g.view(G * N, C, 224, 224)[sel].reshape(2 * C, 224, 224)
     rmaps, _ = wam.subband_maps(p, p.adjoint(gi), 1, 2, C)
     assert float((m.view(G * N, -1)[sel].reshape(-1) - rmaps).abs().max()) <= 2e-6 * float(bmax.max())
+
+
+@pytest.mark.parametrize("wav,n,J,mode", [("db6", 80000, 5, "reflect"), ("haar", 4097, 3, "symmetric"),
+                                          ("sym8", 1001, 4, "zero"), ("db6", 9000, 5, "constant"),
+                                          ("db4", 37, 3, "reflect"), ("db2", 12345, 6, "symmetric"),
+                                          ("coif2", 50000, 4, "reflect")])
+def test_dwt1_tiles_equal_per_axis(wam, wav, n, J, mode):
+    """Fused multi-level 1D tiles (all levels per signal tile in LDS) vs the per-axis kernels, for
+    wavedec, waverec (with IG alphas) and the adjoint; the per-axis path is pinned to pywt above."""
+    fast = wam.get_plan(1, (n,), J, wav, mode, "cuda")
+    gen = wam.get_plan(1, (n,), J, wav, mode, "cuda", generic=True)
+    torch.manual_seed(9)
+    B = 6
+    x = torch.randn(B, n, device="cuda")
+    a, b = fast.wavedec(x), gen.wavedec(x)
+    assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max())
+    ra, rb = fast.waverec(b, B), gen.waverec(b, B)
+    assert torch.equal(ra, rb)  # same per-sample accumulation order as k_synthesis_axis
+    al = [0.0, 0.5, 1.0]
+    assert torch.equal(fast.waverec(b, B, alphas=al), gen.waverec(b, B, alphas=al))
+    g = torch.randn((B,) + fast.rec_shape, device="cuda")
+    a, b = fast.adjoint(g), gen.adjoint(g)
+    assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max())
+
+
+@pytest.mark.parametrize("shape,J,mode", [((128, 128, 128), 2, "symmetric"), ((16, 12, 20), 1, "reflect"),
+                                          ((8, 16, 24), 2, "zero")])
+def test_haar3_blocks_equal_per_axis(wam, shape, J, mode):
+    """Fused 3D Haar blocks (all levels per 2^J block in registers) vs the per-axis kernels:
+    wavedec, waverec (with IG alphas) and the adjoint, bit-identical (same arithmetic order)."""
+    fast = wam.get_plan(3, shape, J, "haar", mode, "cuda")
+    gen = wam.get_plan(3, shape, J, "haar", mode, "cuda", generic=True)
+    torch.manual_seed(10)
+    B = 3
+    x = torch.randn((B,) + shape, device="cuda")
+    a, b = fast.wavedec(x), gen.wavedec(x)
+    assert torch.equal(a, b)
+    assert torch.equal(fast.waverec(b, B), gen.waverec(b, B))
+    al = [0.25, 1.0]
+    assert torch.equal(fast.waverec(b, B, alphas=al), gen.waverec(b, B, alphas=al))
+    g = torch.randn((B,) + fast.rec_shape, device="cuda")
+    assert torch.equal(fast.adjoint(g), gen.adjoint(g))

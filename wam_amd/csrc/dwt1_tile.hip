@@ -1,0 +1,371 @@
+// Fused multi-level 1D transforms for gfx950 (config c3: db6 J=5 on 80,000-sample clips).
+//
+// The per-axis kernels make one HBM round trip per level; here one 256-thread workgroup owns a
+// TILE of one signal and runs all J levels in LDS:
+//   analysis  (wavedec / adjoint of waverec): the tile is a range of coarsest-level outputs; every
+//             finer level computes its own share of outputs plus the halo the next level needs
+//             (recomputed, never exchanged), starting from one window of the source signal loaded
+//             with coalesced loads and the boundary extension applied on the load. Details of each
+//             level's own range go to HBM; the approximation ladder stays in LDS.
+//   synthesis (waverec, IG alpha fused on the load): the tile is a range of output samples; the
+//             coefficient ranges every level needs (own share + filter support) are staged in LDS
+//             and reconstructed coarse to fine; only the finest level writes to HBM.
+// Tiles cover ~4096 source samples, so the recomputed halo ((L-2)(2^J - 1) samples) costs a few
+// percent. Boundary modes: zero, reflect, symmetric, constant (periodic extensions are not local
+// and stay on the per-axis kernels).
+#include <algorithm>
+
+#include "kernels.hpp"
+
+namespace {
+
+constexpr int kT1 = 512;          // threads per workgroup (analysis)
+constexpr int kT1S = 256;         // threads per workgroup (synthesis)
+constexpr int kTile0 = 2048;      // finest-level outputs per tile (source window ~2 x this)
+constexpr int kLds1Cap = 64 * 1024;
+
+struct Dwt1Geom {
+  int J;
+  int mode;
+  int n;                            // input length (level-0 input)
+  int m[WAM_MAX_LEVELS];            // output length of level l (0 = finest)
+  int64_t off_d[WAM_MAX_LEVELS];    // per-item offset of D of level l
+  int64_t off_a;                    // per-item offset of A_J
+  int64_t items;                    // items in the band-major coefficient buffer
+  int tile_j;                       // coarsest-level outputs per tile (analysis)
+  int tiles;                        // tiles per signal
+  int syn_cap;                      // floats per LDS buffer of the synthesis
+};
+
+__host__ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// boundary extension for indices at most one signal length outside [0, n) (the tile halos);
+// farther indices (tiny coarse levels) take the general rule
+__device__ __forceinline__ int ext_near(int i, int n, int mode) {
+  if (i >= 0 && i < n) return i;
+  int r;
+  switch (mode) {
+    case WAM_MODE_ZERO: return -1;
+    case WAM_MODE_CONSTANT: return i < 0 ? 0 : n - 1;
+    case WAM_MODE_REFLECT: r = i < 0 ? -i : 2 * n - 2 - i; break;
+    default: r = i < 0 ? -i - 1 : 2 * n - 1 - i; break;  // symmetric
+  }
+  return (r >= 0 && r < n) ? r : wam_ext_index(i, n, mode);
+}
+
+// ranges (uniform): own [s, e) and computed [S, E) of every level for tile `tile`
+__host__ __device__ __forceinline__ void ana_ranges(const Dwt1Geom& g, int tile, int p, int* S, int* E, int* s,
+                                                    int* e) {
+  const int J = g.J;
+  for (int l = J - 1; l >= 0; --l) {
+    const int T = g.tile_j << (J - 1 - l);
+    const int m = g.m[l];
+    s[l] = tile * T < m ? tile * T : m;
+    e[l] = (tile + 1) * T < m ? (tile + 1) * T : m;
+    int lo = 0x7fffffff, hi = -1;
+    if (s[l] < e[l]) {
+      lo = s[l];
+      hi = e[l];
+    }
+    if (l < J - 1 && S[l + 1] < E[l + 1]) {
+      // taps of level l+1 outputs [S, E): extended indices [a, b] = [2S - p, 2E - 1] of level l
+      const int a = 2 * S[l + 1] - p, b = 2 * E[l + 1] - 1;
+      int nlo = a > 0 ? a : 0, nhi = b < m - 1 ? b : m - 1;
+      if (a < 0) nhi = std::max(nhi, std::min(-a, m - 1));                // single mirror / replicate at 0
+      if (b > m - 1) nlo = std::min(nlo, std::max(0, 2 * (m - 1) - b - 1));  // ... and at m - 1
+      if (a < -(m - 1) || b > 2 * (m - 1)) {                    // several reflections: everything
+        nlo = 0;
+        nhi = m - 1;
+      }
+      if (nlo <= nhi) {
+        lo = std::min(lo, nlo);
+        hi = std::max(hi, nhi + 1);
+      }
+    }
+    S[l] = lo <= hi ? lo : 0;
+    E[l] = lo <= hi ? hi : 0;
+  }
+}
+
+template <int L>
+__global__ void __launch_bounds__(kT1) k_dwt1_ana(const float* __restrict__ in, float* __restrict__ coeffs,
+                                                 const float* __restrict__ filt, Dwt1Geom g) {
+  constexpr int p = L - 2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int64_t item = blockIdx.x / g.tiles;
+  const int tile = (int)(blockIdx.x % g.tiles);
+  float flo[L], fhi[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    flo[k] = filt[k];
+    fhi[k] = filt[L + k];
+  }
+  __shared__ int S[WAM_MAX_LEVELS], E[WAM_MAX_LEVELS], s[WAM_MAX_LEVELS], e[WAM_MAX_LEVELS];
+  if (tid == 0) ana_ranges(g, tile, p, S, E, s, e);
+  __syncthreads();
+  const int J = g.J, mode = g.mode;
+  // LDS (offsets into smem, so every access stays an LDS instruction): source window, then two
+  // approximation buffers. Window = extended indices [2 S0 - p, 2 E0 - 1) of the input.
+  const int w0 = 2 * S[0] - p;
+  const int wlen = 2 * (E[0] - S[0]) + L - 2;
+  const int off_ll0 = (wlen + 63) & ~63;
+  const int off_ll1 = off_ll0 + ((E[0] - S[0] + 63) & ~63);
+  const float* x = in + item * (int64_t)g.n;
+  for (int j = tid; j < wlen; j += kT1) {
+    const int si = ext_near(w0 + j, g.n, mode);
+    smem[j] = si >= 0 ? x[si] : 0.f;
+  }
+  __syncthreads();
+  // level 0 from the window (extension already applied)
+  {
+    const int ml = g.m[0];
+    const bool last = J == 1;
+    float* dout = coeffs + g.items * g.off_d[0] + item * (int64_t)ml;
+    float* aout = coeffs + g.items * g.off_a + item * (int64_t)ml;
+    const int s0 = s[0], e0 = e[0], S0 = S[0], E0 = E[0];
+    for (int i = S0 + tid; i < E0; i += kT1) {
+      const int w = 2 * (i - S0);
+      float a = 0.f, d = 0.f;
+#pragma unroll
+      for (int k = 0; k < L; ++k) {
+        const float v = smem[w + k];
+        a = fmaf(flo[k], v, a);
+        d = fmaf(fhi[k], v, d);
+      }
+      if (i >= s0 && i < e0) {
+        dout[i] = d;
+        if (last) aout[i] = a;
+      }
+      if (!last) smem[off_ll0 + i - S0] = a;
+    }
+    __syncthreads();
+  }
+  // levels 1..J-1 from the approximation buffers (ping-pong by level parity)
+  for (int l = 1; l < J; ++l) {
+    const int ml = g.m[l], nin = g.m[l - 1];
+    const int in_off = (l & 1) ? off_ll0 : off_ll1, out_off = (l & 1) ? off_ll1 : off_ll0;
+    const int base = S[l - 1];
+    const bool last = l == J - 1;
+    float* dout = coeffs + g.items * g.off_d[l] + item * (int64_t)ml;
+    float* aout = coeffs + g.items * g.off_a + item * (int64_t)ml;
+    const int sl = s[l], el = e[l], Sl = S[l], El = E[l];
+    for (int i = Sl + tid; i < El; i += kT1) {
+      const int t0 = 2 * i - p;
+      float a = 0.f, d = 0.f;
+      if (t0 >= 0 && t0 + L - 1 < nin) {
+        const int w = in_off + t0 - base;
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+          const float v = smem[w + k];
+          a = fmaf(flo[k], v, a);
+          d = fmaf(fhi[k], v, d);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+          const int mi = ext_near(t0 + k, nin, mode);
+          const float v = mi >= 0 ? smem[in_off + mi - base] : 0.f;
+          a = fmaf(flo[k], v, a);
+          d = fmaf(fhi[k], v, d);
+        }
+      }
+      if (i >= sl && i < el) {
+        dout[i] = d;
+        if (last) aout[i] = a;
+      }
+      if (!last) smem[out_off + i - Sl] = a;
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// synthesis: tile of level-0 outputs [U0, U1); needed coefficient ranges per level
+__device__ __forceinline__ void syn_ranges(const Dwt1Geom& g, int u0, int u1, int p, int L, int* I0, int* I1) {
+  // (thread 0 only; the ranges are shared through LDS)
+  // level l consumes coefficients [I0[l], I1[l]) to produce outputs [lo, hi) of its output length
+  int lo = u0, hi = u1;
+  for (int l = 0; l < g.J; ++l) {
+    int a = (lo + p - L + 2) >> 1;  // ceil((lo + p - L + 1) / 2)
+    int b = (hi - 1 + p) >> 1;
+    a = max(a, 0);
+    b = min(b, g.m[l] - 1);
+    I0[l] = a;
+    I1[l] = max(a, b + 1);
+    lo = I0[l];
+    hi = I1[l];
+  }
+}
+
+template <int L>
+__global__ void __launch_bounds__(kT1S) k_dwt1_syn(const float* __restrict__ coeffs, float* __restrict__ out,
+                                                 const float* __restrict__ filt, Dwt1Geom g, int nout0, float sc) {
+  constexpr int p = L - 2;
+  constexpr int H2 = L / 2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int64_t item = blockIdx.x / g.tiles;
+  const int tile = (int)(blockIdx.x % g.tiles);
+  float rlo[L], rhi[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    rlo[k] = filt[k];
+    rhi[k] = filt[L + k];
+  }
+  const int u0 = tile * (2 * kTile0), u1 = min(nout0, u0 + 2 * kTile0);
+  __shared__ int I0[WAM_MAX_LEVELS], I1[WAM_MAX_LEVELS];
+  if (tid == 0) syn_ranges(g, u0, u1, p, L, I0, I1);
+  __syncthreads();
+  const int J = g.J;
+  // LDS: two approximation buffers and one detail buffer, each holding a level's coefficient
+  // range [I0 - H2, I1 + H2) with zeros outside [0, m) so every output sums exactly H2 taps
+  const int cap = g.syn_cap;
+  const int off_a[2] = {0, cap};
+  const int off_d = 2 * cap;
+  auto stage = [&](int off, const float* src, int l) {  // src: the level's band for this item
+    const int lo = I0[l] - H2, hi = I1[l] + H2, m = g.m[l];
+    for (int i = lo + tid; i < hi; i += kT1S) smem[off + i - lo] = (i >= 0 && i < m) ? sc * src[i] : 0.f;
+  };
+  stage(off_a[(J - 1) & 1], coeffs + g.items * g.off_a + item * (int64_t)g.m[J - 1], J - 1);
+  for (int l = J - 1; l >= 0; --l) {
+    stage(off_d, coeffs + g.items * g.off_d[l] + item * (int64_t)g.m[l], l);
+    __syncthreads();
+    const int ain = off_a[l & 1];
+    const int lo = I0[l] - H2;
+    const int olo = l ? I0[l - 1] : u0, ohi = l ? I1[l - 1] : u1;
+    const int aout = off_a[(l + 1) & 1];  // == off_a[(l - 1) & 1]
+    float* o = out + item * (int64_t)nout0;
+    for (int u = olo + tid; u < ohi; u += kT1S) {
+      const int t = u + p;  // uncropped position
+      const int ib = t >> 1;
+      const int k0 = t - 2 * ib;
+      float y = 0.f;
+#pragma unroll
+      for (int j = 0; j < H2; ++j) {  // i = ib - j, descending: the order of k_synthesis_axis
+        const int idx = ib - j - lo;
+        y = fmaf(rlo[k0 + 2 * j], smem[ain + idx], y);
+        y = fmaf(rhi[k0 + 2 * j], smem[off_d + idx], y);
+      }
+      if (l) smem[aout + u - olo + H2] = y;  // staged layout of level l-1: index i at i - (I0 - H2)
+      else o[u] = y;
+    }
+    __syncthreads();
+    if (l) {  // zero the pads of the approximation just produced (only ever read outside [0, m))
+      const int plo = I0[l - 1] - H2, phi = I1[l - 1] + H2;
+      for (int i = plo + tid; i < phi; i += kT1S)
+        if (i < I0[l - 1] || i >= I1[l - 1]) smem[aout + i - plo] = 0.f;
+      __syncthreads();
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+bool mode_ok(int mode) { return mode != WAM_MODE_PERIODIC; }
+
+Dwt1Geom make_geom1(const wam_plan* p, int n, int mode, int64_t items) {
+  Dwt1Geom g{};
+  g.J = p->levels;
+  g.mode = mode;
+  g.n = n;
+  for (int l = 0; l < p->levels; ++l) {
+    g.m[l] = (int)p->lout[l][0];
+    g.off_d[l] = p->band_off[wam_band_of(p, l, 0)];
+  }
+  g.off_a = p->band_off[0];
+  g.items = items;
+  g.tile_j = std::max(1, kTile0 >> (p->levels - 1));
+  int tiles = 1;
+  for (int l = 0; l < p->levels; ++l) {
+    const int T = g.tile_j << (p->levels - 1 - l);
+    tiles = std::max(tiles, (g.m[l] + T - 1) / T);
+  }
+  g.tiles = tiles;
+  return g;
+}
+
+// exact LDS of the analysis: the largest window + approximation buffers over all tiles (the
+// first, an interior and the last tiles bound every case; ranges from the device's own rule)
+int ana_lds_bytes(const wam_plan* p, const Dwt1Geom& g) {
+  int best = 0;
+  const int cand[4] = {0, 1, std::max(0, g.tiles - 2), g.tiles - 1};
+  for (int c = 0; c < 4; ++c) {
+    int S[WAM_MAX_LEVELS], E[WAM_MAX_LEVELS], s[WAM_MAX_LEVELS], e[WAM_MAX_LEVELS];
+    ana_ranges(g, cand[c], p->L - 2, S, E, s, e);
+    const int wlen = 2 * (E[0] - S[0]) + p->L - 2;
+    const int need = ((wlen + 63) & ~63) + 2 * ((E[0] - S[0] + 63) & ~63);
+    best = std::max(best, need);
+  }
+  return best * 4;
+}
+
+int syn_lds_bytes(const wam_plan* p) {
+  // level-0 coefficient range of a 2*kTile0 output tile: kTile0 + L/2 (+ the H2 zero pads)
+  const int cap = ((kTile0 + 2 * p->L + 8) + 63) & ~63;
+  return 3 * cap * 4;
+}
+
+}  // namespace
+
+bool dwt1_tile_supported(const wam_plan* p, bool adjoint) {
+  if (p->ndim != 1 || p->L > 20 || (p->L & 1)) return false;
+  if (!mode_ok(adjoint ? WAM_MODE_ZERO : p->mode)) return false;
+  if (p->lin[0][0] > (1 << 30)) return false;
+  const Dwt1Geom g = make_geom1(p, (int)(adjoint ? p->rec_shape[0] : p->lin[0][0]), adjoint ? WAM_MODE_ZERO : p->mode, 1);
+  return ana_lds_bytes(p, g) <= kLds1Cap && syn_lds_bytes(p) <= kLds1Cap;
+}
+
+int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in, float* coeffs, bool adjoint,
+                              hipStream_t st) {
+  if (!dwt1_tile_supported(p, adjoint)) return WAM_ERR_UNSUPPORTED;
+  const int n = (int)(adjoint ? p->rec_shape[0] : p->lin[0][0]);
+  const int mode = adjoint ? WAM_MODE_ZERO : p->mode;
+  const Dwt1Geom g = make_geom1(p, n, mode, batch);
+  const float* filt = p->d_filt + (adjoint ? WAM_F_ADJ_LO : WAM_F_ANA_LO) * p->L;
+  const int64_t blocks = batch * g.tiles;
+  if (blocks > 0x7fffffff) return WAM_ERR_UNSUPPORTED;
+  const int lds = ana_lds_bytes(p, g);
+  WamTimer tm(st, "k_dwt1_ana", 4.0 * (double)batch * ((double)n + (double)p->band_off[p->nbands]));
+  switch (p->L) {
+#define WAM_D1A(LL)                                                                                          \
+  case LL:                                                                                                   \
+    hipLaunchKernelGGL(k_dwt1_ana<LL>, dim3((unsigned)blocks), dim3(kT1), lds, st, in, coeffs, filt, g); \
+    break;
+    WAM_D1A(2) WAM_D1A(4) WAM_D1A(6) WAM_D1A(8) WAM_D1A(10) WAM_D1A(12) WAM_D1A(14) WAM_D1A(16) WAM_D1A(18)
+    WAM_D1A(20)
+#undef WAM_D1A
+    default: return WAM_ERR_UNSUPPORTED;
+  }
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int launch_dwt1_tile_synthesis(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha,
+                               int n_alpha, float* out, hipStream_t st) {
+  if (!dwt1_tile_supported(p, false)) return WAM_ERR_UNSUPPORTED;
+  const int nout = (int)p->rec_shape[0];
+  Dwt1Geom g = make_geom1(p, (int)p->lin[0][0], p->mode, batch);
+  g.tiles = (nout + 2 * kTile0 - 1) / (2 * kTile0);
+  g.syn_cap = syn_lds_bytes(p) / 12;
+  const int64_t blocks = batch * g.tiles;
+  if (blocks > 0x7fffffff) return WAM_ERR_UNSUPPORTED;
+  const float* filt = p->d_filt + WAM_F_SYN_LO * p->L;
+  const int lds = syn_lds_bytes(p);
+  for (int ai = 0; ai < n_alpha; ++ai) {
+    const float sc = alpha ? alpha[ai] : 1.0f;
+    float* o = out + (int64_t)ai * batch * nout;
+    WamTimer tm(st, "k_dwt1_syn", 4.0 * ((double)batch * p->band_off[p->nbands] + (double)batch * (double)nout));
+    switch (p->L) {
+#define WAM_D1S(LL)                                                                                            \
+  case LL:                                                                                                     \
+    hipLaunchKernelGGL(k_dwt1_syn<LL>, dim3((unsigned)blocks), dim3(kT1S), lds, st, coeffs, o, filt, g, nout, sc); \
+    break;
+      WAM_D1S(2) WAM_D1S(4) WAM_D1S(6) WAM_D1S(8) WAM_D1S(10) WAM_D1S(12) WAM_D1S(14) WAM_D1S(16) WAM_D1S(18)
+      WAM_D1S(20)
+#undef WAM_D1S
+      default: return WAM_ERR_UNSUPPORTED;
+    }
+    WAM_LAUNCH_CHECK();
+  }
+  return WAM_OK;
+}

@@ -46,3 +46,17 @@ int launch_dwt2_plane_maps(const wam_plan* p, int64_t images, int channels, int6
 bool dwt2_plane_syn_supported(const wam_plan* p);
 int launch_dwt2_plane_synthesis(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha,
                                 int n_alpha, float* out, hipStream_t st);
+
+// fused multi-level 1D tiles (dwt1_tile.hip)
+bool dwt1_tile_supported(const wam_plan* p, bool adjoint);
+int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in, float* coeffs, bool adjoint,
+                              hipStream_t st);
+int launch_dwt1_tile_synthesis(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha,
+                               int n_alpha, float* out, hipStream_t st);
+
+// fused 3D Haar blocks (dwt3_haar.hip): J <= 2, dims divisible by 2^J
+bool dwt3_haar_supported(const wam_plan* p);
+int launch_dwt3_haar_analysis(const wam_plan* p, int64_t batch, const float* in, float* coeffs, bool adjoint,
+                              hipStream_t st);
+int launch_dwt3_haar_synthesis(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha, int n_alpha,
+                               float* out, hipStream_t st);

@@ -351,6 +351,14 @@ int analysis_driver(const wam_plan* p, int64_t batch, const float* x, float* coe
     int rc = launch_dwt2_plane_analysis(p, batch, x, coeffs, adjoint, noise, n_samples, st);
     if (rc != WAM_ERR_UNSUPPORTED) return rc;
   }
+  if (p->ndim == 1 && !noise && !(p->flags & WAM_PLAN_GENERIC)) {  // all levels per signal tile
+    int rc = launch_dwt1_tile_analysis(p, batch, x, coeffs, adjoint, st);
+    if (rc != WAM_ERR_UNSUPPORTED) return rc;
+  }
+  if (p->ndim == 3 && !noise && !(p->flags & WAM_PLAN_GENERIC)) {  // Haar: all levels per block
+    int rc = launch_dwt3_haar_analysis(p, batch, x, coeffs, adjoint, st);
+    if (rc != WAM_ERR_UNSUPPORTED) return rc;
+  }
   int nd = p->ndim;
   float* w = (float*)ws;
   int64_t ll = batch * wam_prod(p->lout[0], nd);
@@ -461,6 +469,14 @@ int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const flo
   if (p->ndim == 2 && !(p->flags & (WAM_PLAN_GENERIC | WAM_PLAN_NO_ROWS | WAM_PLAN_NO_PLANE)) &&
       dwt2_plane_syn_supported(p)) {  // all levels and all alphas in one launch
     int rc = launch_dwt2_plane_synthesis(p, batch, coeffs, alpha, n_alpha, out, st);
+    if (rc != WAM_ERR_UNSUPPORTED) return rc;
+  }
+  if (p->ndim == 1 && !(p->flags & WAM_PLAN_GENERIC)) {
+    int rc = launch_dwt1_tile_synthesis(p, batch, coeffs, alpha, n_alpha, out, st);
+    if (rc != WAM_ERR_UNSUPPORTED) return rc;
+  }
+  if (p->ndim == 3 && !(p->flags & WAM_PLAN_GENERIC)) {
+    int rc = launch_dwt3_haar_synthesis(p, batch, coeffs, alpha, n_alpha, out, st);
     if (rc != WAM_ERR_UNSUPPORTED) return rc;
   }
   int nd = p->ndim;
