@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--model-dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--sample-batch", type=int, default=4, help="noise samples per model call (x64 images)")
     ap.add_argument("--channels-last", action="store_true", help="NHWC model input (slower with MIOpen here)")
+    ap.add_argument("--no-optimize-model", action="store_true",
+                    help="run the model as is under autocast instead of the BN-folded bf16 copy (model_opt.py)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     return ap.parse_args()
@@ -135,7 +137,7 @@ def main():
     ex = WaveletAttribution2D(model, wavelet="db4", J=3, method="smooth", mode="reflect", n_samples=N_SAMPLES,
                               noise="philox", frame="native", sample_batch=args.sample_batch,
                               autocast_dtype=torch.bfloat16 if args.model_dtype == "bf16" else None,
-                              channels_last=args.channels_last)
+                              channels_last=args.channels_last, optimize_model=not args.no_optimize_model)
 
     def step():
         return ex(x, y)
@@ -199,7 +201,9 @@ def main():
             "config": {"workload": "c2: WAM-2D db4 J=3 SmoothGrad n_samples=25, batch 64 x 224x224, ResNet-50",
                        "model_dtype": args.model_dtype, "global_batch": N_IMAGES * world, "seq_len": None,
                        "parallelism": "dp%d" % world, "noise": "philox", "frame": "native(E1)",
-                       "sample_batch": args.sample_batch, "channels_last": args.channels_last},
+                       "sample_batch": args.sample_batch, "channels_last": args.channels_last,
+                       "model_exec": "autocast" if args.no_optimize_model else
+                       "optimize_model (BN folded into convs, polyphase stem input-gradient, bf16 weights)"},
             "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(line))
     if world > 1:

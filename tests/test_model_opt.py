@@ -1,0 +1,106 @@
+"""wam_amd/model_opt.py: the optimized input-gradient model computes the model's function.
+
+CPU (float64): polyphase input-gradient of stride-2 convs against autograd for odd/even sizes,
+kernel sizes and paddings; BN folding on ResNet-18/50 with randomised running statistics
+(outputs and input gradients). GPU: WAM-2D maps with optimize_model=True vs the model as is.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+import testmodels
+from wam_amd.model_opt import InputConv2d, optimize_for_input_grad
+
+
+def _randomise_bn(model, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    for m in model.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            n = m.num_features
+            m.running_mean.copy_(torch.rand(n, generator=g) - 0.5)
+            m.running_var.copy_(0.5 + 1.5 * torch.rand(n, generator=g))
+            m.weight.data.copy_(0.5 + torch.rand(n, generator=g))
+            m.bias.data.copy_(0.4 * torch.rand(n, generator=g) - 0.2)
+    return model
+
+
+@pytest.mark.parametrize("k,p,h,w", [(7, 3, 224, 224), (7, 3, 31, 30), (3, 1, 17, 16), (4, 1, 20, 21),
+                                     (5, 2, 9, 9), (2, 0, 12, 13), (7, 0, 40, 41), (1, 0, 8, 7)])
+def test_polyphase_input_grad(k, p, h, w):
+    torch.manual_seed(k * 100 + p)
+    conv = nn.Conv2d(3, 8, k, 2, p, bias=True).double()
+    ic = InputConv2d(conv).double()
+    x = torch.randn(2, 3, h, w, dtype=torch.float64, requires_grad=True)
+    y1 = conv(x)
+    go = torch.randn_like(y1)
+    (g1,) = torch.autograd.grad(y1, x, go)
+    x2 = x.detach().requires_grad_(True)
+    y2 = ic(x2)
+    (g2,) = torch.autograd.grad(y2, x2, go)
+    assert torch.equal(y1, y2)
+    assert g2.shape == g1.shape
+    assert (g1 - g2).abs().max().item() <= 1e-13 * max(1.0, g1.abs().max().item())
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_fold_matches_model(arch):
+    m = _randomise_bn(getattr(testmodels, arch)(seed=0)).double()
+    gm = optimize_for_input_grad(m)
+    assert not any(isinstance(q, nn.BatchNorm2d) for q in gm.modules())
+    assert isinstance(gm.conv1, InputConv2d)
+    assert not any(p.requires_grad for p in gm.parameters())
+    x = torch.randn(2, 3, 64, 64, dtype=torch.float64, requires_grad=True)
+    o1 = m(x)
+    (g1,) = torch.autograd.grad(o1[:, 3].sum(), x)
+    x2 = x.detach().requires_grad_(True)
+    o2 = gm(x2)
+    (g2,) = torch.autograd.grad(o2[:, 3].sum(), x2)
+    assert (o1 - o2).abs().max().item() <= 1e-12 * o1.abs().max().item()
+    assert (g1 - g2).abs().max().item() <= 1e-12 * g1.abs().max().item()
+
+
+def test_rejects_training_mode():
+    with pytest.raises(ValueError):
+        optimize_for_input_grad(testmodels.resnet18(seed=0).train())
+
+
+def test_dtype_cast_keeps_polyphase_table():
+    gm = optimize_for_input_grad(testmodels.resnet18(seed=0), dtype=torch.bfloat16)
+    assert gm.conv1.weight.dtype == torch.bfloat16 and gm.conv1.wpoly.dtype == torch.bfloat16
+
+
+class _TinyBN(nn.Module):
+    """Kink-free conv-BN-tanh model: optimized vs original differ only by fp rounding."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv = nn.Conv2d(3, 8, 7, 2, 3, bias=False)
+        self.bn = nn.BatchNorm2d(8)
+        self.conv2 = nn.Conv2d(8, 8, 3, 2, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(8)
+        self.fc = nn.Linear(8 * 4 * 4, 10)
+
+    def forward(self, x):
+        h = torch.tanh(self.bn(self.conv(x)))
+        h = torch.tanh(self.bn2(self.conv2(h)))
+        h = nn.functional.adaptive_avg_pool2d(h, 4)
+        return self.fc(torch.flatten(h, 1))
+
+
+@pytest.mark.gpu
+def test_gpu_wam2d_optimize_model_matches():
+    from wam_amd.wam_2D import WaveletAttribution2D
+    torch.manual_seed(0)
+    m = _TinyBN()
+    for mod in m.modules():
+        if isinstance(mod, nn.BatchNorm2d):
+            mod.running_mean.uniform_(-0.5, 0.5)
+            mod.running_var.uniform_(0.5, 2.0)
+    m = m.eval().cuda()
+    x = torch.tensor(np.random.RandomState(0).standard_normal((2, 3, 64, 64)).astype(np.float32))
+    kw = dict(wavelet="db4", J=3, method="smooth", n_samples=4, noise="philox", frame="native")
+    a = WaveletAttribution2D(m, **kw)(x, [1, 3])
+    b = WaveletAttribution2D(m, optimize_model=True, **kw)(x, [1, 3])
+    assert a.shape == b.shape
+    assert np.abs(a - b).max() <= 1e-4, np.abs(a - b).max()

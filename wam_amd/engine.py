@@ -61,10 +61,12 @@ def seed_gradient(out, y, groups, n):
     return go.to(out.dtype)
 
 
-def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=False, y_none_mean=False):
+def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=False, y_none_mean=False,
+                   input_dtype=None):
     """Gradient of the summed per-group reference losses w.r.t. img (fp32)."""
     img = img.detach().requires_grad_(True)
-    inp = img.contiguous(memory_format=torch.channels_last) if channels_last and img.dim() == 4 else img
+    inp = img if input_dtype is None else img.to(input_dtype)
+    inp = inp.contiguous(memory_format=torch.channels_last) if channels_last and img.dim() == 4 else inp
     ctx = torch.autocast("cuda", dtype=autocast_dtype) if autocast_dtype is not None else contextlib.nullcontext()
     with ctx:
         out = model(inp)
@@ -74,6 +76,38 @@ def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=
     else:
         (g,) = torch.autograd.grad(out, img, grad_outputs=seed_gradient(out, y, groups, n))
     return g.contiguous()
+
+
+class GradModel:
+    """How the explained model is run for its input gradient. optimize=False: the user's model as
+    is (autocast if requested). optimize=True: a traced, BN-folded, frozen copy cast once to
+    autocast_dtype (wam_amd/model_opt.py), built on first use on the model's device."""
+
+    def __init__(self, model, autocast_dtype=None, channels_last=False, optimize=False):
+        self.model = model
+        self.autocast_dtype = autocast_dtype
+        self.channels_last = channels_last
+        self.optimize = optimize
+        self._run = None
+
+    def _runner(self):
+        if self._run is None:
+            if self.optimize:
+                from .model_opt import optimize_for_input_grad
+                run = optimize_for_input_grad(self.model, dtype=self.autocast_dtype)
+                if self.channels_last:
+                    run = run.to(memory_format=torch.channels_last)
+                self._run = run
+            else:
+                self._run = self.model
+        return self._run
+
+    def __call__(self, img, y, groups, n, y_none_mean=False):
+        run = self._runner()
+        if self.optimize:
+            return input_gradient(run, img, y, groups, n, None, self.channels_last, y_none_mean,
+                                  input_dtype=self.autocast_dtype)
+        return input_gradient(run, img, y, groups, n, self.autocast_dtype, self.channels_last, y_none_mean)
 
 
 def legacy_noise(sigmas, item_shape, seed, samples, n_total=None):

@@ -15,6 +15,9 @@ Build-only keyword arguments (all optional, after the reference's own):
   sample_batch   noise samples / IG steps per model call (default: as many as fit 256 images).
   autocast_dtype e.g. torch.bfloat16: run the explained model under autocast (WAM stays fp32).
   channels_last  feed the model NHWC tensors.
+  optimize_model run an eval-mode model as a traced copy with BatchNorm folded into the convs, a
+                 polyphase input-gradient for the stride-2 input conv and weights cast once to
+                 autocast_dtype (wam_amd/model_opt.py); same function up to fp rounding.
   dist           True / ProcessGroup: shard samples (steps) over torch.distributed ranks and
                  all-reduce the accumulated map (RCCL on ROCm); every rank returns the full map.
 """
@@ -24,7 +27,7 @@ import torch.nn.functional as F
 
 from . import frames
 from .constants import WaveletDetailTuple2d
-from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, legacy_noise, model_device,
+from .engine import (GradModel, Shard, auto_group, chunks, ig_weights, legacy_noise, model_device,
                      require_gpu_device, wam_group)
 from .plan import (CAP_ADJOINT_MAPS, CAP_NOISY_WAVEDEC, frame_accumulate, frame_trapz, get_plan, item_sigma,
                    noise_add, reproject_scales, subband_maps)
@@ -86,7 +89,8 @@ class BaseWAM2D:
     """Single gradient pass in the wavelet domain (lib/wam_2D.py:50-264)."""
 
     def __init__(self, model, wavelet="haar", J=3, device=None, mode="reflect", approx_coeffs=False,
-                 normalize_coeffs=True, *, frame="legacy", autocast_dtype=None, channels_last=False):
+                 normalize_coeffs=True, *, frame="legacy", autocast_dtype=None, channels_last=False,
+                 optimize_model=False, _grad=None):
         self.wavelet = wavelet
         self.J = J
         self.mode = mode
@@ -102,6 +106,7 @@ class BaseWAM2D:
         self.frame = frame
         self.autocast_dtype = autocast_dtype
         self.channels_last = channels_last
+        self._grad = _grad if _grad is not None else GradModel(self.model, autocast_dtype, channels_last, optimize_model)
         self._pass = None
         self._wavelet_coeffs = None
         self._gradient_coeffs = None
@@ -203,7 +208,7 @@ class BaseWAM2D:
             bands = [coeffs[0]] + [t for lv in coeffs[1:] for t in lv]
             flat = torch.cat([b.detach().to(dev, torch.float32).reshape(-1) for b in bands])
         img = plan.waverec(flat, n * c)[0].view((n, c) + plan.rec_shape)
-        g = input_gradient(self.model, img, y, 1, n, self.autocast_dtype, self.channels_last)
+        g = self._grad(img, y, 1, n)
         maps, bmax, cg = self._adjoint_maps(plan, g.view((n * c,) + plan.rec_shape), 1, n, c, full=True)
         self._record_pass(plan, flat, cg, n * c, 0, n, c)
         if self.frame == "native":
@@ -268,10 +273,11 @@ class WaveletAttribution2D(BaseWAM2D):
 
     def __init__(self, model, wavelet="haar", method="smooth", J=3, device=None, mode="reflect", approx_coeffs=False,
                  normalize_coeffs=True, n_samples=25, stdev_spread=0.25, random_seed=42, *, noise="numpy",
-                 frame="legacy", sample_batch=None, autocast_dtype=None, channels_last=False, dist=None):
+                 frame="legacy", sample_batch=None, autocast_dtype=None, channels_last=False, dist=None,
+                 optimize_model=False):
         super().__init__(model, wavelet=wavelet, J=J, device=device, mode=mode, approx_coeffs=approx_coeffs,
                          normalize_coeffs=normalize_coeffs, frame=frame, autocast_dtype=autocast_dtype,
-                         channels_last=channels_last)
+                         channels_last=channels_last, optimize_model=optimize_model)
         self.method = method
         self.n_samples = n_samples
         self.stdev_spread = stdev_spread
@@ -283,7 +289,7 @@ class WaveletAttribution2D(BaseWAM2D):
         self.dist = dist
         self.wam = BaseWAM2D(model, wavelet=wavelet, J=J, mode=mode, device=device, approx_coeffs=approx_coeffs,
                              normalize_coeffs=normalize_coeffs, frame=frame, autocast_dtype=autocast_dtype,
-                             channels_last=channels_last)
+                             channels_last=channels_last, _grad=self._grad)
         self._avg_dev = None
 
     # ------------------------------------------------------------------ .scales (lazy)
@@ -309,11 +315,10 @@ class WaveletAttribution2D(BaseWAM2D):
     def _gradients(self, imgs, y, groups, n, model_group):
         """Input gradients of `groups` stacked reference calls, model run `model_group` at a time."""
         if groups <= model_group:
-            return input_gradient(self.model, imgs, y, groups, n, self.autocast_dtype, self.channels_last)
+            return self._grad(imgs, y, groups, n)
         out = torch.empty_like(imgs)
         for s0, cnt in chunks(0, groups, model_group):
-            out[s0 * n:(s0 + cnt) * n] = input_gradient(self.model, imgs[s0 * n:(s0 + cnt) * n], y, cnt, n,
-                                                        self.autocast_dtype, self.channels_last)
+            out[s0 * n:(s0 + cnt) * n] = self._grad(imgs[s0 * n:(s0 + cnt) * n], y, cnt, n)
         return out
 
     def smooth_gradcam(self, x, y):
