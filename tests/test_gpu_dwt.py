@@ -338,3 +338,32 @@ def test_haar3_blocks_equal_per_axis(wam, shape, J, mode):
     assert torch.equal(fast.waverec(b, B, alphas=al), gen.waverec(b, B, alphas=al))
     g = torch.randn((B,) + fast.rec_shape, device="cuda")
     assert torch.equal(fast.adjoint(g), gen.adjoint(g))
+
+
+@pytest.mark.parametrize("wav,shape,J,mode", [("db4", (224, 224), 3, "reflect"), ("haar", (224, 224), 3, "reflect"),
+                                              ("db2", (64, 96), 4, "symmetric"), ("db3", (100, 84), 2, "zero"),
+                                              ("db4", (37, 52), 2, "reflect"), ("sym4", (36, 200), 3, "constant"),
+                                              ("db4", (224, 224), 1, "periodic"), ("db4", (17, 16), 3, "reflect")])
+def test_plane_coop_equals_wave_chunks(wam, wav, shape, J, mode, monkeypatch):
+    """Cooperative level-1 row stream (WAM_PLANE_COOP=1) vs the wave-chunk form (=0): the same
+    taps in the same fma order, so wavedec, noisy wavedec and the maps epilogue are bit-identical."""
+    p = wam.get_plan(2, shape, J, wav, mode, "cuda")
+    if not p.caps & wam.CAP_NOISY_WAVEDEC:
+        pytest.skip("plane kernels do not cover this geometry")
+    torch.manual_seed(11)
+    N, C, S = 3, 3, 4
+    x = torch.randn((N, C) + shape, device="cuda")
+    sigma = wam.item_sigma(x, C * shape[0] * shape[1], C * shape[0] * shape[1], 0.25)
+    g = torch.randn((S * N * C,) + p.rec_shape, device="cuda")
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("WAM_PLANE_COOP", flag)
+        out[flag] = (p.wavedec(x.view(N * C, *shape)),
+                     p.wavedec_noisy(x, sigma, S, N, C, seed=5, sample_base=2),
+                     p.adjoint(g),
+                     p.adjoint_maps(g, S, N, C, full=False)[:2] if p.caps & wam.CAP_ADJOINT_MAPS else ())
+        torch.cuda.synchronize()
+    for a, b in zip(out["0"][:3], out["1"][:3]):
+        assert torch.equal(a, b)
+    for a, b in zip(out["0"][3], out["1"][3]):
+        assert torch.equal(a, b)

@@ -53,6 +53,7 @@ struct PlaneGeom {
   int rowlds;                       // floats per wave-private row
   int llcap;                        // floats of LDS buffer A (LL_1, LL_3, ...)
   int sample_fast;                  // noisy analysis: logical order sample-fastest (1) or plane-fastest (0)
+  int coop;                         // level 1 as the cooperative row stream (COOP kernels)
 };
 
 template <bool MAPS>
@@ -79,17 +80,14 @@ __device__ __forceinline__ float wave_max(float m) {
 
 // MC: 0 = one input plane per item; C > 0 = item is an image of C planes, averaged on load
 // CPL: level-1 output columns per lane (mw <= 64 * CPL): one wave covers a whole row
-template <int L, int CPL, bool NOISE, int MC, bool MAPS>
+// COOP: level 1 as a cooperative row stream (see phase 1 below) instead of wave-private chunks
+template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP>
 __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))) k_plane_ana(const float* __restrict__ in, float* __restrict__ out,
                                                    float* __restrict__ band_max, const float* __restrict__ filt,
                                                    PlaneGeom g, WamNoise nz, int64_t n_items, int64_t S,
                                                    int64_t group_items) {
   constexpr int p = L - 2;
   constexpr int NCH = MC > 0 ? MC : 1;
-  // fetched-row ring: NB-1 rows in flight while one is consumed (C channel rows each); sized
-  // so that the kernel stays within 128 VGPRs (16 waves per CU) without spilling
-  constexpr int NB = CPL > 1 ? 2 : (NCH > 1 ? 3 : 4);
-  constexpr int GRP = (NB % 2 == 0) ? NB : 2 * NB;  // rows per steady-state iteration (even)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ unsigned int wg_max[WAM_MAX_BANDS];
 
@@ -123,11 +121,17 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
   }
   const float* src = in + src_plane * (int64_t)NCH * in_plane;
 
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 fh2[L];  // (lo, hi) tap pairs for packed fp32 FMAs
   float flo[L], fhi[L];
 #pragma unroll
   for (int k = 0; k < L; ++k) {
-    flo[k] = filt[k];
-    fhi[k] = filt[L + k];
+    fh2[k] = f2{filt[k], filt[L + k]};
+    // filter taps live in VGPRs: as 2L scalar registers they push the kernel past the SGPR budget
+    // and the compiler spills uniform values to VGPR lanes (v_readlane + hazard nops per use)
+    asm volatile("" : "+v"(fh2[k]));
+    flo[k] = fh2[k].x;
+    fhi[k] = fh2[k].y;
   }
   if constexpr (MAPS) {
     if (tid < g.nbands) wg_max[tid] = 0u;
@@ -138,7 +142,173 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
   float* bufB = smem + g.llcap;
 
   // ================================================================ phase 1: level 1 (finest)
-  {
+  if constexpr (COOP) {
+    // Cooperative row stream. Extended rows e (ext row e = source row wam_ext_index(e)) are
+    // produced in blocks of 16: wave w fetches rows 16b+2w, 16b+2w+1 (Philox noise / channel
+    // mean applied on the commit to its padded LDS row), filters them horizontally and stores
+    // (lo, hi) per output column into a ring of kRing ext rows; after a barrier the 512 threads
+    // filter vertically: thread (column j, pair q) emits output rows 8b+2q, 8b+2q+1 from 10 ring
+    // rows. Every source row is fetched and noised once (the wave-chunk form re-fetches L-2 halo
+    // rows per wave, 29 % more at 224^2), and the row fetches of the next D-1 blocks stay in
+    // flight in registers across both barriers (plain loads survive __syncthreads()).
+    constexpr int RB = 8;                      // output rows per block
+    constexpr int kRing = 2 * RB + L - 2;      // ext rows a block's vertical pass reads
+    constexpr int D = NCH > 1 ? 1 : 2;         // blocks of row fetches in flight
+    constexpr int PADL = 8;                    // left pad slots (>= p, 16-byte aligned row body)
+    const int mh = g.mh[0], mw = g.mw[0];
+    const int64_t bn = (int64_t)mh * mw;
+    const bool lastlvl = g.J == 1;
+    const int mode = g.mode;
+    const bool zero_mode = mode == WAM_MODE_ZERO;
+    float* wrow = bufB + wv * g.rowlds;
+    float2* ring = reinterpret_cast<float2*>(bufB + kPW * g.rowlds);
+    const PadLane pl = pad_lane(lane, nw, p, mode, PADL);
+    if (zero_mode && pl.dst >= 0) wrow[pl.dst] = 0.f;
+    const int nb = (mh + RB - 1) / RB;
+    float mx[4] = {0.f, 0.f, 0.f, 0.f};
+
+    auto fetch = [&](RowRegs<4, 1> (&fr)[NCH], int& sr_out, int e) {
+      const int sr = row_src(e, nh, mode);
+      const bool valid = sr >= 0;
+      sr_out = sr;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) fr[c].fetch(src + c * in_plane + (int64_t)(valid ? sr : 0) * nw, nw, lane, valid);
+    };
+    // horizontal pass of ext row e into its ring slot
+    auto hrow = [&](RowRegs<4, 1> (&fr)[NCH], int sr, int e) {
+      float nzr[4];
+      if constexpr (NOISE)
+        make_noise<1>(nzr, nw, lane, (ch * nh + (sr >= 0 ? sr : 0)) * (int64_t)nw, sg, img, smp, nz.k0, nz.k1,
+                      sr >= 0);
+      float4 o = fr[0].ok[0] ? make_float4(fr[0].v[0], fr[0].v[1], fr[0].v[2], fr[0].v[3])
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (NCH > 1) {
+#pragma unroll
+        for (int c = 1; c < NCH; ++c) {
+          o.x += fr[c].v[0];
+          o.y += fr[c].v[1];
+          o.z += fr[c].v[2];
+          o.w += fr[c].v[3];
+        }
+        constexpr float inv = 1.0f / (float)NCH;
+        o.x *= inv;
+        o.y *= inv;
+        o.z *= inv;
+        o.w *= inv;
+        if (!fr[0].ok[0]) o = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      if constexpr (NOISE) {
+        o.x = fmaf(sg, nzr[0], o.x);
+        o.y = fmaf(sg, nzr[1], o.y);
+        o.z = fmaf(sg, nzr[2], o.z);
+        o.w = fmaf(sg, nzr[3], o.w);
+      }
+      if (lane * 4 < nw) *reinterpret_cast<float4*>(wrow + PADL + lane * 4) = o;
+      wsync();
+      if (!zero_mode) {
+        refresh_pads(wrow, pl);
+        wsync();
+      }
+      const int slot = (e + p) % kRing;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int j = min(lane + 64 * c, mw - 1);
+        float lo, hi;
+        hfilter<L, PADL>(wrow, j, p, flo, fhi, lo, hi);
+        if (lane + 64 * c < mw) ring[slot * mw + j] = make_float2(lo, hi);
+      }
+      wsync();
+    };
+    // vertical pass of block b: thread (j, q) -> output rows 8b + 2q, 8b + 2q + 1
+    const int vj = tid & 127, vq = tid >> 7;
+    const bool vcol = vj < mw;
+    const int vjc = vcol ? vj : mw - 1;
+    auto vblock = [&](int b) {
+      const int i0 = RB * b + 2 * vq;
+      const int base = (2 * i0) % kRing;  // slot of ext row 2 i0 - p
+      // one pass over the L+2 ring rows feeds both output rows (row 1 starts two rows later);
+      // per accumulator the fma order is tap 0..L-1, as in the wave-chunk form
+      float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int k = 0; k < L + 2; ++k) {
+        int s = base + k;
+        s = s >= kRing ? s - kRing : s;
+        const float2 r = ring[s * mw + vjc];
+        if (k < L) {
+          acc[0][0] = fmaf(flo[k], r.x, acc[0][0]);
+          acc[0][1] = fmaf(fhi[k], r.x, acc[0][1]);
+          acc[0][2] = fmaf(flo[k], r.y, acc[0][2]);
+          acc[0][3] = fmaf(fhi[k], r.y, acc[0][3]);
+        }
+        if (k >= 2) {
+          acc[1][0] = fmaf(flo[k - 2], r.x, acc[1][0]);
+          acc[1][1] = fmaf(fhi[k - 2], r.x, acc[1][1]);
+          acc[1][2] = fmaf(flo[k - 2], r.y, acc[1][2]);
+          acc[1][3] = fmaf(fhi[k - 2], r.y, acc[1][3]);
+        }
+      }
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const float a = acc[h2][0], hh = acc[h2][1], v = acc[h2][2], d = acc[h2][3];
+        const int i = i0 + h2;
+        if (vcol && i < mh) {
+          const int64_t idx = (int64_t)i * mw + vj;
+          if (lastlvl) bo.put(g, g.off_a, bn, idx, a, mx[3]);
+          else bufA[idx] = a;
+          bo.put(g, g.off[0][0], bn, idx, hh, mx[0]);
+          bo.put(g, g.off[0][1], bn, idx, v, mx[1]);
+          bo.put(g, g.off[0][2], bn, idx, d, mx[2]);
+        }
+      }
+    };
+
+    // prologue: ext rows -p .. -1 (waves 0 .. p-1, one each) and the first D blocks in flight
+    RowRegs<4, 1> fp[NCH];
+    int spro;
+    fetch(fp, spro, wv < p ? wv - p : -p);
+    RowRegs<4, 1> F[D][2][NCH];
+    int S[D][2];
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      fetch(F[u][0], S[u][0], 16 * u + 2 * wv);
+      fetch(F[u][1], S[u][1], 16 * u + 2 * wv + 1);
+    }
+    if (wv < p) hrow(fp, spro, wv - p);
+    for (int b0 = 0; b0 < nb; b0 += D) {
+#pragma unroll
+      for (int u = 0; u < D; ++u) {
+        const int b = b0 + u;
+        if (b < nb) {  // workgroup-uniform
+          hrow(F[u][0], S[u][0], 16 * b + 2 * wv);
+          hrow(F[u][1], S[u][1], 16 * b + 2 * wv + 1);
+        }
+        // refill: block b + D (past the plane: clamped rows, never consumed)
+        fetch(F[u][0], S[u][0], 16 * (b + D) + 2 * wv);
+        fetch(F[u][1], S[u][1], 16 * (b + D) + 2 * wv + 1);
+        if (b < nb) {
+          __syncthreads();  // ring rows of block b complete
+          vblock(b);
+          __syncthreads();  // ring slots free for block b + 1
+        }
+      }
+    }
+    if constexpr (MAPS) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mx[b] = wave_max(mx[b]);
+      if (lane == 0) {
+#pragma unroll
+        for (int b = 0; b < 3; ++b) atomicMax(&wg_max[g.band[0][b]], __float_as_uint(mx[b]));
+        if (lastlvl) atomicMax(&wg_max[0], __float_as_uint(mx[3]));
+      }
+    }
+  } else {
+    // Wave chunks: wave w owns output rows [i0, i1) and streams their 2R+L-2 ext rows. Lean
+    // instruction stream (the kernel is VALU-issue bound, profiles/r01f_pmc.txt): the vertical
+    // ring holds (lo, hi) pairs in ring slot t mod L and the loop is unrolled over lcm(L, NBL) rows so
+    // every ring and fetch-buffer index is static (no register rotation); lo/hi and the (a, v) /
+    // (h, d) output pairs are computed with packed fp32 FMAs in the scalar kernels' tap order.
+    constexpr int NBL = (NCH > 1 || CPL > 1) ? 2 : 4;  // fetched rows in registers (NBL - 1 in flight)
+    constexpr int GRPL = (L % NBL == 0) ? L : ((NBL % L == 0) ? NBL : L * NBL / 2);  // lcm(L, NBL)
     const int mh = g.mh[0], mw = g.mw[0];
     const int64_t bn = (int64_t)mh * mw;
     const bool lastlvl = g.J == 1;
@@ -153,9 +323,13 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     const int er0 = 2 * i0 - p;
     const int T = i1 > i0 ? 2 * (i1 - i0) + L - 2 : 0;
     float mx[4] = {0.f, 0.f, 0.f, 0.f};
+    const float2* hsrc[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+      hsrc[c] = reinterpret_cast<const float2*>(lds + kPadL + 2 * min(lane + 64 * c, mw - 1) - p);
 
-    RowRegs<4, 1> f[NB][NCH];
-    int srow[NB];
+    RowRegs<4, 1> f[NBL][NCH];
+    int srow[NBL];
     auto fetch = [&](RowRegs<4, 1> (&fr)[NCH], int& sr_out, int t) {
       const int sr = row_src(er0 + t, nh, mode);
       const bool valid = sr >= 0;
@@ -164,7 +338,8 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
       for (int c = 0; c < NCH; ++c) fr[c].fetch(src + c * in_plane + (int64_t)rr * nw, nw, lane, valid);
     };
-    auto consume = [&](RowRegs<4, 1> (&fr)[NCH], int sr, float (&lo)[CPL], float (&hi)[CPL]) {
+    f2 rv[CPL][L];  // ring: (lo, hi) of ext row t in slot t % L
+    auto consume = [&](RowRegs<4, 1> (&fr)[NCH], int sr, int slot) {
       // the noise depends only on (row, lane): generate it before touching the fetched row so the
       // Philox work overlaps the row's load latency instead of following its vmcnt wait
       float nzr[4];
@@ -191,39 +366,48 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
         refresh_pads(lds, pl);
         wsync();
       }
+      // the CPL columns' accumulation chains interleaved: back-to-back dependent packed FMAs
+      // cost a hazard wait state each
+      f2 acc[CPL];
 #pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        const int j = min(lane + 64 * c, mw - 1);
-        hfilter<L>(lds, j, p, flo, fhi, lo[c], hi[c]);
+      for (int c = 0; c < CPL; ++c) acc[c] = f2{0.f, 0.f};
+#pragma unroll
+      for (int m2 = 0; m2 < L / 2; ++m2) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const float2 x = hsrc[c][m2];
+          acc[c] = __builtin_elementwise_fma(fh2[2 * m2], f2{x.x, x.x}, acc[c]);
+          acc[c] = __builtin_elementwise_fma(fh2[2 * m2 + 1], f2{x.y, x.y}, acc[c]);
+        }
       }
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) rv[c][slot] = acc[c];
       wsync();
     };
-
-    float rl[CPL][L], rh[CPL][L];
-    auto emit = [&](int i) {
+    // output row i from ring slots (s0 + k) % L, k = 0 .. L-1
+    auto emit = [&](int i, int s0) {
+      f2 av[CPL], hd[CPL];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) av[c] = hd[c] = f2{0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < L; ++k) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const f2 r = rv[c][(s0 + k) % L];
+          av[c] = __builtin_elementwise_fma(f2{fh2[k].x, fh2[k].x}, r, av[c]);  // (a, v) = sum flo[k] * (lo, hi)
+          hd[c] = __builtin_elementwise_fma(f2{fh2[k].y, fh2[k].y}, r, hd[c]);  // (h, d) = sum fhi[k] * (lo, hi)
+        }
+      }
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
         const int j = lane + 64 * c;
-        float a = 0.f, h = 0.f, v = 0.f, d = 0.f;
-#pragma unroll
-        for (int k = 0; k < L; ++k) {
-          a = fmaf(flo[k], rl[c][k], a);
-          h = fmaf(fhi[k], rl[c][k], h);
-          v = fmaf(flo[k], rh[c][k], v);
-          d = fmaf(fhi[k], rh[c][k], d);
-        }
         if (j < mw && i < i1) {
           const int64_t idx = (int64_t)i * mw + j;
-          if (lastlvl) bo.put(g, g.off_a, bn, idx, a, mx[3]);
-          else bufA[idx] = a;
-          bo.put(g, g.off[0][0], bn, idx, h, mx[0]);
-          bo.put(g, g.off[0][1], bn, idx, v, mx[1]);
-          bo.put(g, g.off[0][2], bn, idx, d, mx[2]);
-        }
-#pragma unroll
-        for (int k = 0; k < L - 2; ++k) {
-          rl[c][k] = rl[c][k + 2];
-          rh[c][k] = rh[c][k + 2];
+          if (lastlvl) bo.put(g, g.off_a, bn, idx, av[c].x, mx[3]);
+          else bufA[idx] = av[c].x;
+          bo.put(g, g.off[0][0], bn, idx, hd[c].x, mx[0]);
+          bo.put(g, g.off[0][1], bn, idx, av[c].y, mx[1]);
+          bo.put(g, g.off[0][2], bn, idx, hd[c].y, mx[2]);
         }
       }
     };
@@ -233,36 +417,24 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     // join, serialising the row stream on memory latency.
     if (T > 0) {
 #pragma unroll
-      for (int u = 0; u < NB - 1; ++u) fetch(f[u], srow[u], u);
+      for (int u = 0; u < NBL - 1; ++u) fetch(f[u], srow[u], u);
       // prologue: ext rows 0 .. L-3 fill ring slots 0 .. L-3
 #pragma unroll
       for (int t = 0; t < L - 2; ++t) {
-        fetch(f[(t + NB - 1) % NB], srow[(t + NB - 1) % NB], t + NB - 1);
-        float lo[CPL], hi[CPL];
-        consume(f[t % NB], srow[t % NB], lo, hi);
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          rl[c][t] = lo[c];
-          rh[c][t] = hi[c];
-        }
+        fetch(f[(t + NBL - 1) % NBL], srow[(t + NBL - 1) % NBL], t + NBL - 1);
+        consume(f[t % NBL], srow[t % NBL], t);
       }
-      // steady state: GRP ext rows (GRP/2 output rows) per iteration, static ring-buffer indices;
-      // a partial last group computes output rows >= i1, which emit() drops
-      for (int base = L - 2; base < T; base += GRP) {
+      // steady state: GRPL ext rows per iteration; t = base + u with base = L-2 (mod GRPL), so
+      // t % L and t % NBL are compile-time constants; a partial last group computes output rows
+      // >= i1, which emit() drops
+      for (int base = L - 2; base < T; base += GRPL) {
 #pragma unroll
-        for (int u = 0; u < GRP; ++u) {
+        for (int u = 0; u < GRPL; ++u) {
           const int t = base + u;
-          const int fb = (L - 2 + u + NB - 1) % NB;
-          fetch(f[fb], srow[fb], t + NB - 1);
-          float lo[CPL], hi[CPL];
-          consume(f[(L - 2 + u) % NB], srow[(L - 2 + u) % NB], lo, hi);
-          const int slot = (u & 1) ? L - 1 : L - 2;
-#pragma unroll
-          for (int c = 0; c < CPL; ++c) {
-            rl[c][slot] = lo[c];
-            rh[c][slot] = hi[c];
-          }
-          if (u & 1) emit(i0 + (t - (L - 1)) / 2);
+          fetch(f[(L - 2 + u + NBL - 1) % NBL], srow[(L - 2 + u + NBL - 1) % NBL], t + NBL - 1);
+          consume(f[(L - 2 + u) % NBL], srow[(L - 2 + u) % NBL], (L - 2 + u) % L);
+          // after odd u: output row (t - (L-1)) / 2 from ext rows t-L+1 .. t = slots (u-1+k) % L
+          if (u & 1) emit(i0 + (t - (L - 1)) / 2, (u - 1) % L);
         }
       }
     }
@@ -568,7 +740,32 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
 // whose register ring of L rows x 2 columns x lo/hi does not fit the 128-VGPR budget of 16 waves/CU
 bool l_ok(int L) { return L == 2 || L == 4 || L == 6 || L == 8; }
 
+// cooperative level 1 (COOP): wave rows with 8 left pad slots + a ring of 2*8+L-2 (lo, hi) rows;
+// chosen when two workgroups still fit a CU (the ring replaces the wave-chunk halo re-fetch)
+constexpr int kCoopPadL = 8;
+constexpr int kTwoWgLds = 160 * 1024 / 2 - 4 * WAM_MAX_BANDS - 64;  // minus the static wg_max table
+
+int coop_lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap) {
+  rowlds = (kCoopPadL + nw0 + p->pad + (nw0 & 1) + 1 + 3) & ~3;
+  llcap = p->levels > 1 ? (int)((p->lout[0][0] * p->lout[0][1] + 63) & ~63) : 0;
+  int64_t bcap = (int64_t)kPW * rowlds + 2 * (16 + p->L - 2) * p->lout[0][1];
+  if (p->levels > 1) {
+    const int64_t ll2 = p->lout[1][0] * p->lout[1][1];
+    if (ll2 > bcap) bcap = ll2;
+  }
+  return (int)(llcap + bcap);
+}
+
+bool coop_ok(const wam_plan* p, int nw0) {
+  const char* e = getenv("WAM_PLANE_COOP");
+  if (e && e[0] == '0') return false;
+  if (p->lout[0][1] > 128 || p->pad > kCoopPadL) return false;
+  int rowlds, llcap;
+  return (int64_t)coop_lds_floats(p, nw0, rowlds, llcap) * 4 <= kTwoWgLds || (e && e[0] == '1');
+}
+
 int lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap) {
+  if (coop_ok(p, nw0)) return coop_lds_floats(p, nw0, rowlds, llcap);
   rowlds = kPadL + 256 + 8;  // commit covers 256 samples; pads <= p + 2 <= 20 fit behind them
   if (rowlds < kPadL + nw0 + p->pad + 4) rowlds = kPadL + nw0 + p->pad + 4;
   rowlds = (rowlds + 3) & ~3;
@@ -612,16 +809,17 @@ PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items
   g.items_total = items_total;
   g.maps_item = p->band_off[p->nbands];
   lds_floats(p, nw0, g.rowlds, g.llcap);
+  g.coop = coop_ok(p, nw0);
   const char* o = getenv("WAM_NOISE_ORDER");
   g.sample_fast = !(o && o[0] == 'p');
   return g;
 }
 
-template <int L, int CPL, bool NOISE, int MC, bool MAPS>
+template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP>
 int launch_plane_t(const PlaneGeom& g, int lds_bytes, int64_t n_items, const float* in, float* out, float* band_max,
                    const float* filt, const WamNoise& nz, int64_t S, int64_t group_items, const char* name,
                    double bytes, hipStream_t st) {
-  auto kern = k_plane_ana<L, CPL, NOISE, MC, MAPS>;
+  auto kern = k_plane_ana<L, CPL, NOISE, MC, MAPS, COOP>;
   static std::atomic<uint64_t> attr_set{0};  // opt in to > 64 KB of dynamic LDS, once per device
   int dev = 0;
   WAM_HIP_CHECK(hipGetDevice(&dev));
@@ -643,17 +841,20 @@ int dispatch_plane(const wam_plan* p, const PlaneGeom& g, int lds_bytes, int64_t
                    float* out, float* band_max, const float* filt, const WamNoise& nz, int64_t S,
                    int64_t group_items, const char* name, double bytes, hipStream_t st) {
   const bool two = g.mw[0] > 64;
+#define WAM_PLANE_ARGS g, lds_bytes, n_items, in, out, band_max, filt, nz, S, group_items, name, bytes, st
 #define WAM_PLANE_CASE(LL)                                                                                       \
   case LL:                                                                                                       \
-    return two ? launch_plane_t<LL, 2, NOISE, MC, MAPS>(g, lds_bytes, n_items, in, out, band_max, filt, nz, S,    \
-                                                        group_items, name, bytes, st)                            \
-               : launch_plane_t<LL, 1, NOISE, MC, MAPS>(g, lds_bytes, n_items, in, out, band_max, filt, nz, S,    \
-                                                        group_items, name, bytes, st);
+    if (g.coop)                                                                                                  \
+      return two ? launch_plane_t<LL, 2, NOISE, MC, MAPS, true>(WAM_PLANE_ARGS)                                  \
+                 : launch_plane_t<LL, 1, NOISE, MC, MAPS, true>(WAM_PLANE_ARGS);                                 \
+    return two ? launch_plane_t<LL, 2, NOISE, MC, MAPS, false>(WAM_PLANE_ARGS)                                   \
+               : launch_plane_t<LL, 1, NOISE, MC, MAPS, false>(WAM_PLANE_ARGS);
   switch (p->L) {
     WAM_PLANE_CASE(2) WAM_PLANE_CASE(4) WAM_PLANE_CASE(6) WAM_PLANE_CASE(8)
     default: return WAM_ERR_UNSUPPORTED;
   }
 #undef WAM_PLANE_CASE
+#undef WAM_PLANE_ARGS
 }
 
 }  // namespace

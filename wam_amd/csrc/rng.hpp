@@ -20,6 +20,10 @@ __device__ __forceinline__ wam_u4 wam_philox4x32_10(wam_u4 c, uint32_t k0, uint3
     c = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += W0;
     k1 += W1;
+    // keep the key schedule as two scalar registers advanced by SALU adds: folded into 20
+    // constants it exceeds the SGPR budget of the plane kernels and is spilled to VGPR lanes
+    // (one v_readlane + hazard nop per use)
+    asm volatile("" : "+s"(k0), "+s"(k1));
   }
   return c;
 }

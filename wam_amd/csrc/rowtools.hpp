@@ -94,16 +94,16 @@ struct PadLane {
   int src;   // lds index of its source sample (or -1: zero)
 };
 
-__device__ __forceinline__ PadLane pad_lane(int lane, int nw, int p, int mode) {
+__device__ __forceinline__ PadLane pad_lane(int lane, int nw, int p, int mode, int padl = kPadL) {
   const int npad_r = p + (nw & 1) + 1;  // right pads (one spare)
   PadLane pl{-1, -1};
   int e;
   if (lane < p) e = lane - p;
   else if (lane < p + npad_r) e = nw + (lane - p);
   else return pl;
-  pl.dst = kPadL + e;
+  pl.dst = padl + e;
   const int s = wam_ext_index(e, nw, mode);
-  pl.src = s >= 0 ? kPadL + s : -1;
+  pl.src = s >= 0 ? padl + s : -1;
   return pl;
 }
 
@@ -115,10 +115,10 @@ __device__ __forceinline__ void refresh_pads(float* lds, const PadLane& pl) {
 }
 
 // Horizontal analysis of output column j from the padded LDS row (ext column 2j - p + k).
-template <int L>
+template <int L, int PADL = kPadL>
 __device__ __forceinline__ void hfilter(const float* lds, int j, int p, const float (&flo)[L], const float (&fhi)[L],
                                         float& lo, float& hi) {
-  const float2* s2 = reinterpret_cast<const float2*>(lds + kPadL + 2 * j - p);  // even offset (p even)
+  const float2* s2 = reinterpret_cast<const float2*>(lds + PADL + 2 * j - p);  // even offset (p, PADL even)
   float a = 0.f, d = 0.f;
 #pragma unroll
   for (int k = 0; k < L; k += 2) {
