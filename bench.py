@@ -48,8 +48,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model-dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--sample-batch", type=int, default=4, help="noise samples per model call (x64 images)")
-    ap.add_argument("--channels-last", action="store_true", help="NHWC model input (slower with MIOpen here)")
+    ap.add_argument("--sample-batch", type=int, default=13, help="noise samples per model call (x64 images)")
+    ap.add_argument("--channels-last", dest="channels_last", action="store_true", default=True,
+                    help="NHWC model execution (default; faster than NCHW for the BN-folded bf16 model)")
+    ap.add_argument("--no-channels-last", dest="channels_last", action="store_false")
     ap.add_argument("--no-optimize-model", action="store_true",
                     help="run the model as is under autocast instead of the BN-folded bf16 copy (model_opt.py)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
