@@ -205,6 +205,26 @@ int wam_trapz_f32(int64_t groups, int64_t k0, int64_t len, const float* src, con
 int wam_reproject_scales(int64_t items, int size, int levels, int approx, const double* avg,
                          double* out, void* stream);
 
+/* ------------------------------------------------------------------------------------------------
+ * Explained-model input-gradient pass (lib/wam_2D.py:114-116: model forward, diag-mean loss,
+ * backward). Not a ptwt replacement: fused elementwise steps of a BN-folded ReLU network, each one
+ * HBM pass instead of the 2-4 torch kernels it replaces (wam_amd/model_fuse.py drives them).
+ * dtype: WAM_DT_F32 or WAM_DT_BF16 (storage; arithmetic is fp32). Tensors are contiguous with n
+ * elements; the channel of element i is (i / inner) % channels (inner = 1: NHWC, H*W: NCHW).
+ * Bias vectors (length channels, same dtype) may be NULL (= 0). out may alias an input.
+ * ---------------------------------------------------------------------------------------------- */
+enum wam_dtype { WAM_DT_F32 = 0, WAM_DT_BF16 = 1 };
+
+/* y = relu ? max(y + bias[c], 0) : y + bias[c]      (in place; conv bias + ReLU) */
+int wam_ew_bias_act(int dtype, int64_t n, int64_t channels, int64_t inner, void* y, const void* bias,
+                    int relu, void* stream);
+/* out = max((a + bias_a[c]) + (s + bias_s[c]), 0)   (residual tail of a bottleneck block) */
+int wam_ew_add_bias_relu(int dtype, int64_t n, int64_t channels, int64_t inner, const void* a,
+                         const void* bias_a, const void* s, const void* bias_s, void* out, void* stream);
+/* out = y > 0 ? g1 (+ g2 if g2 != NULL) : 0          (ReLU backward, optionally fused fan-in) */
+int wam_ew_relu_mask(int dtype, int64_t n, const void* g1, const void* g2, const void* y, void* out,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

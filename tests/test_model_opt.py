@@ -104,3 +104,88 @@ def test_gpu_wam2d_optimize_model_matches():
     b = WaveletAttribution2D(m, optimize_model=True, **kw)(x, [1, 3])
     assert a.shape == b.shape
     assert np.abs(a - b).max() <= 1e-4, np.abs(a - b).max()
+
+
+# ------------------------------------------------------------------ fused elementwise (model_fuse)
+def test_fuse_rewrite_structure():
+    """The graph rewrite (CPU, no compute): every conv->ReLU, the stem and every residual tail of
+    ResNet-50 become fused modules; no ReLU, add or biased conv is left on the pattern."""
+    import operator
+    from wam_amd import model_fuse
+    gm = optimize_for_input_grad(testmodels.resnet50(seed=0), fuse=False)
+    gm, n = model_fuse.fuse_elementwise(gm)
+    assert n == 1 + 16 * 2 + 16
+    kinds = [type(m).__name__ for m in gm.modules()]
+    assert kinds.count("ConvBiasReLU") == 32 and kinds.count("AddBiasReLU") == 16
+    assert kinds.count("InputConvReLU") == 1 and kinds.count("ConvNoBias") == 16 + 4
+    assert "ReLU" not in kinds
+    assert not any(nd.op == "call_function" and nd.target is operator.add for nd in gm.graph.nodes)
+    gm18, n18 = model_fuse.fuse_elementwise(optimize_for_input_grad(testmodels.resnet18(seed=0), fuse=False))
+    assert n18 == 1 + 8 + 8
+
+
+def test_fuse_not_applied_on_cpu():
+    gm = optimize_for_input_grad(testmodels.resnet18(seed=0))
+    assert not any(type(m).__name__ == "ConvBiasReLU" for m in gm.modules())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cl", [False, True])
+def test_gpu_ew_kernels_match_torch(dtype, cl):
+    from wam_amd import model_fuse as mf
+    torch.manual_seed(0)
+    for shape in [(3, 64, 14, 14), (2, 24, 7, 7), (2, 5, 3, 3), (4, 256, 8, 8)]:
+        mk = lambda: torch.randn(shape, device="cuda").to(dtype)  # noqa: E731
+        y, a, s, g, g2 = mk(), mk(), mk(), mk(), mk()
+        if cl:
+            y, a, s, g, g2 = (t.contiguous(memory_format=torch.channels_last) for t in (y, a, s, g, g2))
+        b1 = torch.randn(shape[1], device="cuda").to(dtype)
+        b2 = torch.randn(shape[1], device="cuda").to(dtype)
+        bc = lambda b: b.float().view(1, -1, 1, 1)  # noqa: E731
+        ref = torch.relu(y.float() + bc(b1)).to(dtype)
+        out = mf.bias_act_(y.clone(memory_format=torch.preserve_format), b1, True)
+        assert torch.equal(out, ref)
+        ref = torch.relu((a.float() + bc(b1)) + (s.float() + bc(b2))).to(dtype)
+        assert torch.equal(mf.add_bias_relu(a, b1, s, b2), ref)
+        assert torch.equal(mf.add_bias_relu(a, None, s, None), torch.relu(a.float() + s.float()).to(dtype))
+        assert torch.equal(mf.relu_mask(g, y), torch.where(y > 0, g, torch.zeros_like(g)))
+        assert torch.equal(mf.relu_mask(g, y, g2), torch.where(y > 0, (g.float() + g2.float()).to(dtype),
+                                                                 torch.zeros_like(g)))
+        # mixed layouts: gradient NCHW, activation NHWC
+        assert torch.equal(mf.relu_mask(g.contiguous(), y), torch.where(y > 0, g, torch.zeros_like(g)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arch,dtype,cl", [("resnet50", torch.float32, False), ("resnet50", torch.bfloat16, True),
+                                           ("resnet18", torch.bfloat16, False), ("resnet50", torch.float32, True)])
+def test_gpu_fused_model_matches_unfused(arch, dtype, cl):
+    """Fused input-gradient model vs the same folded model op by op, both against the model in
+    float64 on the CPU: the fused form must be as close to the exact gradient as the unfused one
+    (ReLU masks can flip on rounding-level differences, so the two GPU forms are not compared
+    with each other at a fixed tolerance)."""
+    m = _randomise_bn(getattr(testmodels, arch)(seed=0))
+    torch.manual_seed(1)
+    x = torch.randn(4, 3, 96, 96)
+    x64 = x.double().requires_grad_(True)
+    o64 = m.double()(x64)
+    (g64,) = torch.autograd.grad(o64[:, 7].sum(), x64)
+    m = m.float().cuda()
+    ref = optimize_for_input_grad(m, dtype=dtype, fuse=False)
+    fus = optimize_for_input_grad(m, dtype=dtype, fuse=True)
+    assert any(type(q).__name__ == "AddBiasReLU" for q in fus.modules())
+    fmt = torch.channels_last if cl else torch.contiguous_format
+    ref, fus = ref.to(memory_format=fmt), fus.to(memory_format=fmt)
+    xd = x.cuda().to(dtype).contiguous(memory_format=fmt)
+    errs = []
+    for net in (ref, fus):
+        xx = xd.detach().requires_grad_(True)
+        o = net(xx)
+        (g,) = torch.autograd.grad(o[:, 7].float().sum(), xx)
+        oe = ((o.double().cpu() - o64.detach()).abs().max() / o64.abs().max()).item()
+        ge = ((g.double().cpu() - g64).norm() / g64.norm()).item()
+        errs.append((oe, ge))
+    (oe_r, ge_r), (oe_f, ge_f) = errs
+    floor = 1e-5 if dtype == torch.float32 else 1e-2
+    assert oe_f <= 2 * oe_r + floor, errs
+    assert ge_f <= 2 * ge_r + floor, errs

@@ -57,6 +57,9 @@ _SIGS = {
     "wam_wavedec_noisy": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, ctypes.c_uint64, c_i64, c_vp, c_vp, c_vp]),
     "wam_waverec_adjoint_maps": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "wam_timing_enable": (c_int, [c_int]),
+    "wam_ew_bias_act": (c_int, [c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_int, c_vp]),
+    "wam_ew_add_bias_relu": (c_int, [c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "wam_ew_relu_mask": (c_int, [c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "wam_timing_drain": (c_int, [c_int, ctypes.c_char_p, ctypes.POINTER(c_f32), ctypes.POINTER(ctypes.c_double)]),
 }
 

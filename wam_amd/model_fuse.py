@@ -1,0 +1,306 @@
+"""Fused elementwise execution of a BN-folded ReLU network's input-gradient pass.
+
+After ``model_opt`` folds BatchNorm into the convolutions, a ResNet input-gradient step is
+convolutions (MIOpen, MFMA) plus per-channel bias adds, ReLUs, residual adds and ReLU masks.
+Executed op by op in torch these elementwise steps are separate HBM passes over activation
+tensors -- on MI355X about half of the c2 step (profiles/r01f_bench_kernel_stats.csv: torch
+add / clamp / threshold_backward kernels next to the convolutions). ``fuse_elementwise``
+rewrites the traced graph so each chain is one HIP kernel (wam_amd/csrc/model_ew.hip):
+
+* ``conv -> relu``            -> ``ConvBiasReLU``: the convolution without bias, then
+  y = max(y + b, 0) in place; backward = ReLU mask (one pass) + convolution backward-data.
+* ``relu(a + s)`` where a / s are biased convolutions (bottleneck tail, downsample shortcut)
+  -> the convolutions without bias and ``AddBiasReLU``: out = max((a + b_a) + (s + b_s), 0) in
+  one pass; backward = one ReLU-mask pass whose result feeds both branches.
+* the polyphase input convolution (``model_opt.InputConv2d``) followed by a ReLU gets the same
+  bias + ReLU epilogue and a masked polyphase backward.
+
+Only the pattern's own nodes are touched; everything else runs as traced. The functions are the
+same as the graph's up to fp rounding (the bf16 tail sum rounds once instead of three times);
+tests/test_model_opt.py compares outputs and input gradients with the unfused model on the GPU.
+There is no CPU path for the fused ops: on a CPU model the rewrite is not applied.
+"""
+import operator
+
+import torch
+import torch.fx as fx
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from .model_opt import InputConv2d, _PolyphaseInputGrad  # noqa: F401
+
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+def _dt(t):
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError("wam_amd fused model ops support float32 / bfloat16 activations, got %s" % t.dtype)
+
+
+def _layout(t):
+    """(tensor in a dense layout, inner) where the channel of flat element i is (i // inner) % C."""
+    if t.dim() == 4 and t.shape[1] > 1 and t.shape[2] * t.shape[3] > 1:
+        if t.is_contiguous(memory_format=torch.channels_last):
+            return t, 1
+        t = t.contiguous()
+        return t, t.shape[2] * t.shape[3]
+    t = t.contiguous()
+    inner = 1
+    for d in t.shape[2:]:
+        inner *= d
+    return t, inner
+
+
+def _like(t, ref):
+    """t in ref's memory layout (dense), so flat elementwise indexing lines up."""
+    if ref.dim() == 4 and ref.is_contiguous(memory_format=torch.channels_last) and not ref.is_contiguous():
+        return t.contiguous(memory_format=torch.channels_last)
+    return t.contiguous()
+
+
+def _stream(t):
+    return _lib.c_vp(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def bias_act_(y, b, relu=True):
+    y, inner = _layout(y)
+    _lib.check(_lib.lib.wam_ew_bias_act(_dt(y), y.numel(), y.shape[1], inner, _lib.ptr(y),
+                                        _lib.ptr(b.to(y.dtype).contiguous() if b is not None else None),
+                                        int(relu), _stream(y)))
+    return y
+
+
+def add_bias_relu(a, ba, s, bs):
+    a, inner = _layout(a)
+    s = _like(s, a)
+    out = torch.empty_like(a)
+    cast = (lambda b: None if b is None else b.to(a.dtype).contiguous())
+    _lib.check(_lib.lib.wam_ew_add_bias_relu(_dt(a), a.numel(), a.shape[1], inner, _lib.ptr(a), _lib.ptr(cast(ba)),
+                                             _lib.ptr(s), _lib.ptr(cast(bs)), _lib.ptr(out), _stream(a)))
+    return out
+
+
+def relu_mask(g, y, g2=None):
+    """y > 0 ? g (+ g2) : 0 in y's layout."""
+    g = _like(g, y)
+    g2 = None if g2 is None else _like(g2, y)
+    out = torch.empty_like(y)
+    _lib.check(_lib.lib.wam_ew_relu_mask(_dt(y), y.numel(), _lib.ptr(g), _lib.ptr(g2), _lib.ptr(y), _lib.ptr(out),
+                                         _stream(y)))
+    return out
+
+
+def _conv_nd(x, w, stride, padding, dilation, groups):
+    return torch.ops.aten.convolution(x, w, None, stride, padding, dilation, False, [0] * len(stride), groups)
+
+
+def _conv_grad_input(g, x, w, stride, padding, dilation, groups):
+    return torch.ops.aten.convolution_backward(g, x, w, None, stride, padding, dilation, False, [0] * len(stride),
+                                               groups, [True, False, False])[0]
+
+
+class _ConvBiasReLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, geom):
+        y = bias_act_(_conv_nd(x, w, *geom), b, True)
+        ctx.save_for_backward(x, w, y)
+        ctx.geom = geom
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, y = ctx.saved_tensors
+        return _conv_grad_input(relu_mask(g, y), x, w, *ctx.geom), None, None, None
+
+
+class _AddBiasReLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, ba, s, bs):
+        out = add_bias_relu(a, ba, s, bs)
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (out,) = ctx.saved_tensors
+        gm = relu_mask(g, out)
+        return gm, None, gm, None
+
+
+class _PolyphaseReLUFn(torch.autograd.Function):
+    """relu(InputConv2d(x)): conv without bias + fused bias/ReLU; backward = mask + polyphase."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, wpoly, pad, geom):
+        y = bias_act_(F.conv2d(x, weight, None, 2, pad), bias, True)
+        ctx.save_for_backward(wpoly, y)
+        ctx.geom = geom
+        ctx.in_hw = x.shape[-2:]
+        return y
+
+    @staticmethod
+    def backward(ctx, go):
+        wpoly, y = ctx.saved_tensors
+        gm = relu_mask(go, y)
+
+        class _C:  # reuse the polyphase backward with its saved table
+            saved_tensors = (wpoly,)
+            geom = ctx.geom
+            in_hw = ctx.in_hw
+        return _PolyphaseInputGrad.backward(_C, gm)
+
+
+def _geom(conv):
+    return (list(conv.stride), list(conv.padding), list(conv.dilation), conv.groups)
+
+
+class ConvBiasReLU(nn.Module):
+    """relu(conv(x)) for a frozen, zero-padded Conv1d/2d/3d with bias (one fused epilogue)."""
+
+    def __init__(self, conv):
+        super().__init__()
+        self.weight = nn.Parameter(conv.weight.detach().clone(), requires_grad=False)
+        b = conv.bias.detach().clone() if conv.bias is not None else torch.zeros(conv.out_channels)
+        self.bias = nn.Parameter(b, requires_grad=False)
+        self.geom = _geom(conv)
+
+    def forward(self, x):
+        return _ConvBiasReLUFn.apply(x, self.weight, self.bias, self.geom)
+
+
+class ConvNoBias(nn.Module):
+    """conv(x) with its bias moved into the consumer (AddBiasReLU)."""
+
+    def __init__(self, conv):
+        super().__init__()
+        self.weight = nn.Parameter(conv.weight.detach().clone(), requires_grad=False)
+        self.geom = _geom(conv)
+
+    def forward(self, x):
+        return _conv_nd(x, self.weight, *self.geom)
+
+
+class AddBiasReLU(nn.Module):
+    """relu((a + bias_a) + (s + bias_s)) -- residual tail; biases may be absent."""
+
+    def __init__(self, bias_a=None, bias_s=None):
+        super().__init__()
+        self.bias_a = None if bias_a is None else nn.Parameter(bias_a.detach().clone(), requires_grad=False)
+        self.bias_s = None if bias_s is None else nn.Parameter(bias_s.detach().clone(), requires_grad=False)
+
+    def forward(self, a, s):
+        return _AddBiasReLUFn.apply(a, self.bias_a, s, self.bias_s)
+
+
+class InputConvReLU(nn.Module):
+    """relu(InputConv2d(x)) with the fused bias/ReLU epilogue and masked polyphase backward."""
+
+    def __init__(self, ic):
+        super().__init__()
+        self.ic = ic
+
+    def forward(self, x):
+        from .model_opt import _phase_geometry
+        ic = self.ic
+        H, W = x.shape[-2:]
+        oy, Ty, _, ny = _phase_geometry(ic.kh, ic.pad[0], H)
+        ox, Tx, _, nx = _phase_geometry(ic.kw, ic.pad[1], W)
+        b = ic.bias if ic.bias is not None else torch.zeros(ic.weight.shape[0], dtype=ic.weight.dtype,
+                                                            device=ic.weight.device)
+        return _PolyphaseReLUFn.apply(x, ic.weight, b, ic.wpoly, ic.pad, ((oy, Ty, ny), (ox, Tx, nx)))
+
+
+# --------------------------------------------------------------------------------- graph rewrite
+_RELU_FN = (F.relu, torch.relu)
+
+
+def _is_relu(node, mods):
+    if node.op == "call_module":
+        m = mods.get(node.target)
+        return type(m) is nn.ReLU
+    if node.op == "call_function":
+        return node.target in _RELU_FN and len(node.args) == 1
+    if node.op == "call_method":
+        return node.target in ("relu", "relu_") and len(node.args) == 1
+    return False
+
+
+def _fusable_conv(node, mods):
+    if node.op != "call_module" or len(node.users) != 1:
+        return None
+    m = mods.get(node.target)
+    if type(m) in (nn.Conv1d, nn.Conv2d, nn.Conv3d) and m.padding_mode == "zeros" and not isinstance(m.padding, str):
+        return m
+    return None
+
+
+def fuse_elementwise(gm):
+    """Rewrite a traced (BN-folded, frozen) GraphModule in place; returns it and the fusion count."""
+    mods = dict(gm.named_modules())
+    g = gm.graph
+    count = 0
+    uid = [0]
+
+    def add_mod(prefix, m):
+        uid[0] += 1
+        name = "%s_wamfuse%d" % (prefix.replace(".", "_"), uid[0])
+        gm.add_submodule(name, m)
+        mods[name] = m
+        return name
+
+    for node in list(g.nodes):
+        if not _is_relu(node, mods):
+            continue
+        src = node.args[0]
+        if not isinstance(src, fx.Node) or len(src.users) != 1:
+            continue
+        conv = _fusable_conv(src, mods)
+        if conv is not None:  # conv -> relu
+            name = add_mod(src.target, ConvBiasReLU(conv))
+            with g.inserting_before(node):
+                new = g.call_module(name, (src.args[0],))
+            node.replace_all_uses_with(new)
+            g.erase_node(node)
+            g.erase_node(src)
+            count += 1
+            continue
+        if src.op == "call_module" and isinstance(mods.get(src.target), InputConv2d):  # input conv -> relu
+            name = add_mod(src.target, InputConvReLU(mods[src.target]))
+            with g.inserting_before(node):
+                new = g.call_module(name, (src.args[0],))
+            node.replace_all_uses_with(new)
+            g.erase_node(node)
+            g.erase_node(src)
+            count += 1
+            continue
+        if src.op == "call_function" and src.target in (operator.add, torch.add) and len(src.args) == 2 \
+                and not src.kwargs and all(isinstance(a, fx.Node) for a in src.args):
+            operands, biases, drop = [], [], []
+            for a in src.args:
+                c = _fusable_conv(a, mods)
+                if c is not None and c.bias is not None:
+                    cname = add_mod(a.target, ConvNoBias(c))
+                    with g.inserting_before(a):
+                        na = g.call_module(cname, (a.args[0],))
+                    operands.append(na)
+                    biases.append(c.bias)
+                    drop.append(a)
+                else:
+                    operands.append(a)
+                    biases.append(None)
+            name = add_mod("add_relu", AddBiasReLU(*biases))
+            with g.inserting_before(node):
+                new = g.call_module(name, tuple(operands))
+            node.replace_all_uses_with(new)
+            g.erase_node(node)
+            g.erase_node(src)
+            for a in drop:
+                g.erase_node(a)
+            count += 1
+    g.lint()
+    gm.recompile()
+    gm.delete_all_unused_submodules()
+    return gm, count

@@ -147,8 +147,10 @@ def _set_module(root, target, new):
     setattr(root.get_submodule(parent) if parent else root, name, new)
 
 
-def optimize_for_input_grad(model, dtype=None, fold_bn=True, input_conv=True):
-    """A traced, frozen copy of an eval-mode `model` computing the same function (see module doc)."""
+def optimize_for_input_grad(model, dtype=None, fold_bn=True, input_conv=True, fuse=None):
+    """A traced, frozen copy of an eval-mode `model` computing the same function (see module doc).
+    fuse: rewrite conv/bias/ReLU/residual chains into the fused HIP epilogues (model_fuse.py);
+    None = when the model lives on the GPU (and WAM_MODEL_FUSE is not 0)."""
     if model.training:
         raise ValueError("optimize_for_input_grad needs an eval-mode model (BatchNorm folding uses running stats)")
     try:
@@ -185,6 +187,13 @@ def optimize_for_input_grad(model, dtype=None, fold_bn=True, input_conv=True):
     gm.graph.lint()
     gm.recompile()
     gm.delete_all_unused_submodules()
+    if fuse is None:
+        import os
+        dev = next((p.device for p in gm.parameters()), torch.device("cpu"))
+        fuse = dev.type == "cuda" and os.environ.get("WAM_MODEL_FUSE", "1") != "0"
+    if fuse:
+        from .model_fuse import fuse_elementwise
+        gm, _ = fuse_elementwise(gm)
     gm.eval()
     if dtype is not None:
         gm = gm.to(dtype)
