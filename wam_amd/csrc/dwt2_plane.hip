@@ -97,7 +97,9 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
   const int64_t lwg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
   if (lwg >= n_items) return;  // never taken (grid == n_items); keeps the barrier count uniform
 
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // the wave index is wave-uniform: readfirstlane puts it (and every row index, ring slot and
+  // Philox counter word derived from it) in SGPRs, so row bookkeeping runs on the scalar unit
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nh = g.nh0, nw = g.nw0;
   const int64_t in_plane = (int64_t)nh * nw;
 
@@ -210,17 +212,30 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
         wsync();
       }
       const int slot = (e + p) % kRing;
+      // (lo, hi) of the CPL columns as packed FMAs, per accumulator in tap order 0..L-1 (the
+      // wave-chunk form's order); the CPL chains interleaved to hide the packed-FMA hazard
+      f2 acc[CPL];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) acc[c] = f2{0.f, 0.f};
+#pragma unroll
+      for (int m2 = 0; m2 < L / 2; ++m2) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const int j = min(lane + 64 * c, mw - 1);
+          const float2 x = reinterpret_cast<const float2*>(wrow + PADL + 2 * j - p)[m2];
+          acc[c] = __builtin_elementwise_fma(fh2[2 * m2], f2{x.x, x.x}, acc[c]);
+          acc[c] = __builtin_elementwise_fma(fh2[2 * m2 + 1], f2{x.y, x.y}, acc[c]);
+        }
+      }
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
         const int j = min(lane + 64 * c, mw - 1);
-        float lo, hi;
-        hfilter<L, PADL>(wrow, j, p, flo, fhi, lo, hi);
-        if (lane + 64 * c < mw) ring[slot * mw + j] = make_float2(lo, hi);
+        if (lane + 64 * c < mw) ring[slot * mw + j] = make_float2(acc[c].x, acc[c].y);
       }
       wsync();
     };
     // vertical pass of block b: thread (j, q) -> output rows 8b + 2q, 8b + 2q + 1
-    const int vj = tid & 127, vq = tid >> 7;
+    const int vj = tid & 127, vq = __builtin_amdgcn_readfirstlane(tid >> 7);  // wave-uniform
     const bool vcol = vj < mw;
     const int vjc = vcol ? vj : mw - 1;
     auto vblock = [&](int b) {
@@ -228,28 +243,25 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
       const int base = (2 * i0) % kRing;  // slot of ext row 2 i0 - p
       // one pass over the L+2 ring rows feeds both output rows (row 1 starts two rows later);
       // per accumulator the fma order is tap 0..L-1, as in the wave-chunk form
-      float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      // packed FMAs: (a, h) += (flo, fhi) * lo and (v, d) += (flo, fhi) * hi
+      f2 ah[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}}, vd[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
 #pragma unroll
       for (int k = 0; k < L + 2; ++k) {
         int s = base + k;
         s = s >= kRing ? s - kRing : s;
         const float2 r = ring[s * mw + vjc];
         if (k < L) {
-          acc[0][0] = fmaf(flo[k], r.x, acc[0][0]);
-          acc[0][1] = fmaf(fhi[k], r.x, acc[0][1]);
-          acc[0][2] = fmaf(flo[k], r.y, acc[0][2]);
-          acc[0][3] = fmaf(fhi[k], r.y, acc[0][3]);
+          ah[0] = __builtin_elementwise_fma(fh2[k], f2{r.x, r.x}, ah[0]);
+          vd[0] = __builtin_elementwise_fma(fh2[k], f2{r.y, r.y}, vd[0]);
         }
         if (k >= 2) {
-          acc[1][0] = fmaf(flo[k - 2], r.x, acc[1][0]);
-          acc[1][1] = fmaf(fhi[k - 2], r.x, acc[1][1]);
-          acc[1][2] = fmaf(flo[k - 2], r.y, acc[1][2]);
-          acc[1][3] = fmaf(fhi[k - 2], r.y, acc[1][3]);
+          ah[1] = __builtin_elementwise_fma(fh2[k - 2], f2{r.x, r.x}, ah[1]);
+          vd[1] = __builtin_elementwise_fma(fh2[k - 2], f2{r.y, r.y}, vd[1]);
         }
       }
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
-        const float a = acc[h2][0], hh = acc[h2][1], v = acc[h2][2], d = acc[h2][3];
+        const float a = ah[h2].x, hh = ah[h2].y, v = vd[h2].x, d = vd[h2].y;
         const int i = i0 + h2;
         if (vcol && i < mh) {
           const int64_t idx = (int64_t)i * mw + vj;

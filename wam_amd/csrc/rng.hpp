@@ -17,7 +17,9 @@ __device__ __forceinline__ wam_u4 wam_philox4x32_10(wam_u4 c, uint32_t k0, uint3
     const uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    c = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    // three-input xor as one v_bitop3_b32 (truth table 0x96; gfx950) instead of two v_xor_b32
+    c = {(uint32_t)__builtin_amdgcn_bitop3_b32(hi1, c.y, k0, 0x96), lo1,
+         (uint32_t)__builtin_amdgcn_bitop3_b32(hi0, c.w, k1, 0x96), lo0};
     k0 += W0;
     k1 += W1;
     // keep the key schedule as two scalar registers advanced by SALU adds: folded into 20
