@@ -161,12 +161,14 @@ def test_gpu_ew_kernels_match_torch(dtype, cl):
                                            ("resnet18", torch.bfloat16, False), ("resnet50", torch.float32, True)])
 def test_gpu_fused_model_matches_unfused(arch, dtype, cl):
     """Fused input-gradient model vs the same folded model op by op, both against the model in
-    float64 on the CPU: the fused form must be as close to the exact gradient as the unfused one
-    (ReLU masks can flip on rounding-level differences, so the two GPU forms are not compared
-    with each other at a fixed tolerance)."""
+    float64 on the CPU: the fused form must be as close to the exact gradient as the unfused one.
+    ReLU masks flip on rounding-level differences (measured on MI355X, scripts/gemm_check.py: one
+    96^2 batch of 4 in 5 flips a mask in the MIOpen path as well as in the GEMM path, moving that
+    batch's gradient by ~4e-3 relative), so the gradients are compared per image by the median
+    over 8 images, with a bound on the worst image that a real layout or indexing error exceeds."""
     m = _randomise_bn(getattr(testmodels, arch)(seed=0))
     torch.manual_seed(1)
-    x = torch.randn(4, 3, 96, 96)
+    x = torch.randn(8, 3, 96, 96)
     x64 = x.double().requires_grad_(True)
     o64 = m.double()(x64)
     (g64,) = torch.autograd.grad(o64[:, 7].sum(), x64)
@@ -183,9 +185,11 @@ def test_gpu_fused_model_matches_unfused(arch, dtype, cl):
         o = net(xx)
         (g,) = torch.autograd.grad(o[:, 7].float().sum(), xx)
         oe = ((o.double().cpu() - o64.detach()).abs().max() / o64.abs().max()).item()
-        ge = ((g.double().cpu() - g64).norm() / g64.norm()).item()
-        errs.append((oe, ge))
-    (oe_r, ge_r), (oe_f, ge_f) = errs
+        d = (g.double().cpu() - g64).flatten(1).norm(dim=1) / g64.flatten(1).norm(dim=1)
+        errs.append((oe, d.median().item(), d.max().item()))
+    (oe_r, ge_r, _), (oe_f, ge_f, gmax_f) = errs
     floor = 1e-5 if dtype == torch.float32 else 1e-2
+    worst = 5e-2 if dtype == torch.float32 else 0.5
     assert oe_f <= 2 * oe_r + floor, errs
     assert ge_f <= 2 * ge_r + floor, errs
+    assert gmax_f <= worst, errs
