@@ -120,8 +120,14 @@ def test_fuse_rewrite_structure():
     assert kinds.count("InputConvReLU") == 1 and kinds.count("ConvNoBias") == 16 + 4
     assert "ReLU" not in kinds
     assert not any(nd.op == "call_function" and nd.target is operator.add for nd in gm.graph.nodes)
+    # identity blocks (16 minus the 4 with a downsample) hand their skip gradient to the
+    # producing block's ReLU mask
+    assert sum(getattr(m, "link_in", None) is not None for m in gm.modules()) == 12
+    assert sum(getattr(m, "link_out", None) is not None for m in gm.modules()) == 12
     gm18, n18 = model_fuse.fuse_elementwise(optimize_for_input_grad(testmodels.resnet18(seed=0), fuse=False))
     assert n18 == 1 + 8 + 8
+    # resnet18: layer1.0 takes the max-pool output (no producing add), so 5 - 1 links
+    assert sum(getattr(m, "link_in", None) is not None for m in gm18.modules()) == 4
 
 
 def test_fuse_not_applied_on_cpu():

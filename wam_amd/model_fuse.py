@@ -135,6 +135,33 @@ def _addmm_relu(b, x2, w2t):
         return torch.relu_(torch.addmm(b, x2, w2t))
 
 
+class _SkipGrad:
+    """Hand-off of a residual block's skip-path gradient to the block that produced its input.
+
+    In a ResNet identity block the input x (the previous block's AddBiasReLU output) feeds both
+    conv1 and the residual add, so autograd would sum the two gradients of x in a separate
+    elementwise pass before the producer's ReLU mask (8 % of the c2 step). Instead the add
+    receives x detached and parks its skip gradient here, and the producer's backward, which
+    autograd runs later (it is upstream of both users), applies its mask to the sum in one kernel
+    (relu_mask(g, y, g2)). One box per forward call: the producer's forward opens it and the
+    consumer's forward takes it, so repeated forwards before a backward stay separate. Measured:
+    adding the skip gradient as the C operand of conv1's input-gradient GEMM instead gains nothing
+    (torch.addmm copies C into the output first; scripts/skip_ab.py)."""
+
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+
+class _SkipLink:
+    """Link between a producer AddBiasReLU and the consumer AddBiasReLU that takes its output as
+    the skip operand."""
+
+    def __init__(self):
+        self.cur = None
+
+
 class _ConvBiasReLUFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, geom):
@@ -184,16 +211,23 @@ class _PointwiseConvFn(torch.autograd.Function):
 
 class _AddBiasReLUFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, ba, s, bs):
+    def forward(ctx, a, ba, s, bs, park=None, take=None):
         out = add_bias_relu(a, ba, s, bs)
         ctx.save_for_backward(out)
+        ctx.park, ctx.take = park, take
         return out
 
     @staticmethod
     def backward(ctx, g):
         (out,) = ctx.saved_tensors
-        gm = relu_mask(g, out)
-        return gm, None, gm, None
+        g2 = None
+        if ctx.take is not None:  # skip gradient of the consumer block, summed under the mask
+            g2, ctx.take.g = ctx.take.g, None
+        gm = relu_mask(g, out, g2)
+        if ctx.park is not None:  # s was passed detached: its gradient goes to s's producer
+            ctx.park.g = gm
+            return gm, None, None, None, None, None
+        return gm, None, gm, None, None, None
 
 
 class _PolyphaseReLUFn(torch.autograd.Function):
@@ -233,6 +267,7 @@ class ConvBiasReLU(nn.Module):
         self.bias = nn.Parameter(b, requires_grad=False)
         self.geom = _geom(conv)
 
+
     def forward(self, x):
         return _ConvBiasReLUFn.apply(x, self.weight, self.bias, self.geom)
 
@@ -262,8 +297,18 @@ class AddBiasReLU(nn.Module):
         self.bias_a = None if bias_a is None else nn.Parameter(bias_a.detach().clone(), requires_grad=False)
         self.bias_s = None if bias_s is None else nn.Parameter(bias_s.detach().clone(), requires_grad=False)
 
+        self.link_in = None   # _SkipLink: operand s comes from a linked producer (park its gradient)
+        self.link_out = None  # _SkipLink: this output is a linked consumer's skip operand (take it)
+
     def forward(self, a, s):
-        return _AddBiasReLUFn.apply(a, self.bias_a, s, self.bias_s)
+        park = take = None
+        if self.link_in is not None and self.link_in.cur is not None and torch.is_grad_enabled():
+            park, self.link_in.cur = self.link_in.cur, None
+            s = s.detach()
+        if self.link_out is not None:
+            grad = torch.is_grad_enabled() and (a.requires_grad or s.requires_grad)
+            take = self.link_out.cur = _SkipGrad() if grad else None
+        return _AddBiasReLUFn.apply(a, self.bias_a, s, self.bias_s, park, take)
 
 
 class InputConvReLU(nn.Module):
@@ -371,7 +416,28 @@ def fuse_elementwise(gm):
             for a in drop:
                 g.erase_node(a)
             count += 1
+    _link_skip_gradients(gm, mods)
     g.lint()
     gm.recompile()
     gm.delete_all_unused_submodules()
     return gm, count
+
+
+def _link_skip_gradients(gm, mods):
+    """Link each identity residual block's AddBiasReLU with the AddBiasReLU that produced its skip
+    operand, when that output has exactly two users: the block's conv1 and the add (_SkipGrad)."""
+    links = 0
+    for node in gm.graph.nodes:
+        if node.op != "call_module" or type(mods.get(node.target)) is not AddBiasReLU:
+            continue
+        users = list(node.users)
+        if len(users) != 2:
+            continue
+        add = [u for u in users if u.op == "call_module" and type(mods.get(u.target)) is AddBiasReLU]
+        if len(add) != 1 or len(add[0].args) != 2 or add[0].args[1] is not node or add[0].args[0] is node:
+            continue
+        link = _SkipLink()
+        mods[node.target].link_out = link
+        mods[add[0].target].link_in = link
+        links += 1
+    return links
