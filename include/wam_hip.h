@@ -224,6 +224,16 @@ int wam_ew_add_bias_relu(int dtype, int64_t n, int64_t channels, int64_t inner, 
 /* out = y > 0 ? g1 (+ g2 if g2 != NULL) : 0          (ReLU backward, optionally fused fan-in) */
 int wam_ew_relu_mask(int dtype, int64_t n, const void* g1, const void* g2, const void* y, void* out,
                      void* stream);
+/* NHWC max pooling (k x k window, stride, zero-area padding pad <= k/2, floor output size):
+ * y [n, ho, wo, c], idx [n, ho, wo, c] uint8 = window position kh*k+kw | 0x80 if the max is > 0.
+ * Replaces torch max_pool2d_with_indices after the stem ReLU (torchvision ResNet maxpool);
+ * WAM_ERR_UNSUPPORTED when c is not a multiple of the 16-byte vector or pointers are unaligned. */
+int wam_ew_maxpool_nhwc(int dtype, int64_t n, int64_t h, int64_t w, int64_t c, int k, int stride, int pad,
+                        const void* x, void* y, void* idx, void* stream);
+/* gx [n, h, w, c] = sum of gy over the windows whose idx points at the pixel (fp32 sums in window
+ * order); relu != 0 also drops windows whose max was not > 0 (mask of the ReLU feeding the pool). */
+int wam_ew_maxpool_nhwc_backward(int dtype, int64_t n, int64_t h, int64_t w, int64_t c, int k, int stride,
+                                 int pad, const void* gy, const void* idx, int relu, void* gx, void* stream);
 
 #ifdef __cplusplus
 }

@@ -114,10 +114,11 @@ def test_fuse_rewrite_structure():
     from wam_amd import model_fuse
     gm = optimize_for_input_grad(testmodels.resnet50(seed=0), fuse=False)
     gm, n = model_fuse.fuse_elementwise(gm)
-    assert n == 1 + 16 * 2 + 16
+    assert n == 1 + 16 * 2 + 16 + 1
     kinds = [type(m).__name__ for m in gm.modules()]
     assert kinds.count("ConvBiasReLU") == 32 and kinds.count("AddBiasReLU") == 16
-    assert kinds.count("InputConvReLU") == 1 and kinds.count("ConvNoBias") == 16 + 4
+    assert kinds.count("InputConvReLUPool") == 1 and kinds.count("ConvNoBias") == 16 + 4
+    assert "MaxPool2d" not in kinds and "InputConvReLU" not in kinds
     assert "ReLU" not in kinds
     assert not any(nd.op == "call_function" and nd.target is operator.add for nd in gm.graph.nodes)
     # identity blocks (16 minus the 4 with a downsample) hand their skip gradient to the
@@ -125,7 +126,7 @@ def test_fuse_rewrite_structure():
     assert sum(getattr(m, "link_in", None) is not None for m in gm.modules()) == 12
     assert sum(getattr(m, "link_out", None) is not None for m in gm.modules()) == 12
     gm18, n18 = model_fuse.fuse_elementwise(optimize_for_input_grad(testmodels.resnet18(seed=0), fuse=False))
-    assert n18 == 1 + 8 + 8
+    assert n18 == 1 + 8 + 8 + 1
     # resnet18: layer1.0 takes the max-pool output (no producing add), so 5 - 1 links
     assert sum(getattr(m, "link_in", None) is not None for m in gm18.modules()) == 4
 
@@ -160,6 +161,32 @@ def test_gpu_ew_kernels_match_torch(dtype, cl):
                                                                  torch.zeros_like(g)))
         # mixed layouts: gradient NCHW, activation NHWC
         assert torch.equal(mf.relu_mask(g.contiguous(), y), torch.where(y > 0, g, torch.zeros_like(g)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("k,st,p,h,w,c", [(3, 2, 1, 112, 112, 64), (3, 2, 1, 17, 14, 16), (2, 2, 0, 9, 8, 8),
+                                          (3, 1, 1, 7, 6, 24)])
+def test_gpu_maxpool_nhwc_matches_torch(dtype, k, st, p, h, w, c):
+    """Byte-index NHWC max pool vs torch max_pool2d(_with_indices) and its backward: pooled values
+    bit-equal, input gradient bit-equal (fp32 sums of <= 4 window terms in the same order), and
+    with relu=True equal to torch's backward followed by the ReLU mask of the pooled input.
+    Ties and exact zeros (ReLU outputs) are forced by quantising half of the input to 0."""
+    from wam_amd import model_fuse as mf
+    torch.manual_seed(3)
+    y = torch.relu(torch.randn(3, c, h, w, device="cuda")).to(dtype)
+    y = torch.where(torch.rand_like(y, dtype=torch.float32) < 0.3, torch.zeros_like(y), y)
+    y = y.contiguous(memory_format=torch.channels_last)
+    out, idx = mf.maxpool_nhwc(y, k, st, p)
+    ref, ridx = torch.nn.functional.max_pool2d(y.float(), k, st, p, return_indices=True)
+    assert torch.equal(out.float(), ref)
+    go = torch.randn_like(ref).to(dtype).contiguous(memory_format=torch.channels_last)
+    gref = torch.ops.aten.max_pool2d_with_indices_backward(go.float(), y.float(), [k, k], [st, st], [p, p], [1, 1],
+                                                           False, ridx)
+    g0 = mf.maxpool_nhwc_backward(go, idx, y.shape, k, st, p, relu=False)
+    assert torch.allclose(g0.float(), gref.to(dtype).float(), rtol=0, atol=0)
+    g1 = mf.maxpool_nhwc_backward(go, idx, y.shape, k, st, p, relu=True)
+    assert torch.equal(g1.float(), torch.where(y.float() > 0, gref, torch.zeros_like(gref)).to(dtype).float())
 
 
 @pytest.mark.gpu

@@ -60,6 +60,9 @@ _SIGS = {
     "wam_ew_bias_act": (c_int, [c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_int, c_vp]),
     "wam_ew_add_bias_relu": (c_int, [c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "wam_ew_relu_mask": (c_int, [c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "wam_ew_maxpool_nhwc": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "wam_ew_maxpool_nhwc_backward": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp,
+                                             c_int, c_vp, c_vp]),
     "wam_timing_drain": (c_int, [c_int, ctypes.c_char_p, ctypes.POINTER(c_f32), ctypes.POINTER(ctypes.c_double)]),
 }
 

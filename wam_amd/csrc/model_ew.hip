@@ -10,6 +10,8 @@
 //   k_add_bias_relu out = relu(a + ba[c] + s + bs[c])          (bottleneck tail + residual)
 //   k_relu_mask     out = y > 0 ? g : 0                        (ReLU backward)
 //   k_add_relu_mask out = y > 0 ? g1 + g2 : 0                  (gradient fan-in + ReLU backward)
+//   k_maxpool_fwd / k_maxpool_bwd  NHWC max pooling with a byte window index; the backward
+//                   also applies the mask of the ReLU that fed the pool (stem relu -> maxpool)
 // Arithmetic in fp32, storage fp32 or bf16 (round to nearest even on the store). Every kernel
 // moves 16 bytes per access (8 bf16 / 4 fp32) with UNR accesses in flight per thread; the channel
 // of an element is (i / inner) % C (inner = 1 for NHWC, H*W for NCHW).
@@ -269,6 +271,147 @@ int relu_mask(int64_t n, const void* g1_, const void* g2_, const void* y_, void*
   return WAM_OK;
 }
 
+
+// ---- max pooling over a channels_last (NHWC) activation, window index kept as one byte
+// Forward: one thread per (n, oy, ox, 16-byte channel vector); max in window scan order with
+// torch's rule (first maximum wins, NaN propagates, the index of an all -inf window is its first
+// valid position). idx = window position kh * k + kw, bit 7 set when the maximum is > 0 -- the
+// ReLU that produced the input is then folded into the backward (a ReLU output is 0 wherever the
+// mask would cut the gradient, and a window whose maximum is 0 routes its gradient to a zero).
+// Backward (gather, no atomics): one thread per input vector sums, in (oy, ox) order and in fp32,
+// the gradients of the <= ceil(k/s)^2 windows whose recorded position is this pixel -- torch's
+// max_pool2d backward order. The byte index replaces torch's int64 one: 8x less index traffic.
+struct PoolGeom {
+  int64_t n, h, w, c, ho, wo;
+  int k, s, p;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(kBlk) k_maxpool_fwd(PoolGeom g, const T* __restrict__ x, T* __restrict__ y,
+                                                        uint8_t* __restrict__ idx) {
+  constexpr int V = Vec<T>::N;
+  typedef typename Vec<T>::raw R;
+  const int64_t cv = g.c / V;
+  const int64_t total = g.n * g.ho * g.wo * cv;
+  const int64_t q = (int64_t)blockIdx.x * kBlk + threadIdx.x;
+  if (q >= total) return;
+  int64_t r = q / cv;
+  const int64_t c0 = (q - r * cv) * V;
+  const int64_t ox = r % g.wo;
+  r /= g.wo;
+  const int64_t oy = r % g.ho;
+  const int64_t n = r / g.ho;
+  const int64_t y0 = oy * g.s - g.p, x0 = ox * g.s - g.p;
+  const int ky0 = (int)max<int64_t>(0, -y0), ky1 = (int)min<int64_t>(g.k, g.h - y0);
+  const int kx0 = (int)max<int64_t>(0, -x0), kx1 = (int)min<int64_t>(g.k, g.w - x0);
+  float m[V];
+  int id[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) m[j] = -INFINITY, id[j] = ky0 * g.k + kx0;
+  for (int ky = ky0; ky < ky1; ++ky) {
+    const T* row = x + ((n * g.h + y0 + ky) * g.w) * g.c + c0;
+    for (int kx = kx0; kx < kx1; ++kx) {
+      float v[V];
+      Vec<T>::unpack(*reinterpret_cast<const R*>(row + (x0 + kx) * g.c), v);
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+        if (v[j] > m[j] || isnan(v[j])) m[j] = v[j], id[j] = ky * g.k + kx;
+    }
+  }
+  const int64_t o = ((n * g.ho + oy) * g.wo + ox) * g.c + c0;
+  *reinterpret_cast<R*>(y + o) = Vec<T>::pack(m);
+  uint8_t b[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) b[j] = (uint8_t)(id[j] | (m[j] > 0.f ? 0x80 : 0));
+  if constexpr (V == 8) {
+    uint2 w;
+    w.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+    w.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
+    *reinterpret_cast<uint2*>(idx + o) = w;
+  } else {
+    *reinterpret_cast<uint32_t*>(idx + o) = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+  }
+}
+
+template <typename T, bool RELU>
+__global__ void __launch_bounds__(kBlk) k_maxpool_bwd(PoolGeom g, const T* __restrict__ gy,
+                                                        const uint8_t* __restrict__ idx, T* __restrict__ gx) {
+  constexpr int V = Vec<T>::N;
+  typedef typename Vec<T>::raw R;
+  const int64_t cv = g.c / V;
+  const int64_t total = g.n * g.h * g.w * cv;
+  const int64_t q = (int64_t)blockIdx.x * kBlk + threadIdx.x;
+  if (q >= total) return;
+  int64_t r = q / cv;
+  const int64_t c0 = (q - r * cv) * V;
+  const int64_t ix = r % g.w;
+  r /= g.w;
+  const int64_t iy = r % g.h;
+  const int64_t n = r / g.h;
+  // windows oy with oy*s - p <= iy <= oy*s - p + k - 1
+  const int64_t oy0 = max<int64_t>(0, (iy + g.p - g.k + g.s) / g.s), oy1 = min<int64_t>(g.ho - 1, (iy + g.p) / g.s);
+  const int64_t ox0 = max<int64_t>(0, (ix + g.p - g.k + g.s) / g.s), ox1 = min<int64_t>(g.wo - 1, (ix + g.p) / g.s);
+  float acc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) acc[j] = 0.f;
+  for (int64_t oy = oy0; oy <= oy1; ++oy) {
+    const int py = (int)(iy - (oy * g.s - g.p));
+    for (int64_t ox = ox0; ox <= ox1; ++ox) {
+      const int pos = py * g.k + (int)(ix - (ox * g.s - g.p));
+      const int64_t o = ((n * g.ho + oy) * g.wo + ox) * g.c + c0;
+      float v[V];
+      Vec<T>::unpack(*reinterpret_cast<const R*>(gy + o), v);
+      uint8_t b[V];
+      if constexpr (V == 8) {
+        const uint2 w = *reinterpret_cast<const uint2*>(idx + o);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = (uint8_t)(w.x >> (8 * j)), b[4 + j] = (uint8_t)(w.y >> (8 * j));
+      } else {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(idx + o);
+#pragma unroll
+        for (int j = 0; j < V; ++j) b[j] = (uint8_t)(w >> (8 * j));
+      }
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+        if ((b[j] & 0x7f) == pos && (!RELU || (b[j] & 0x80))) acc[j] += v[j];
+    }
+  }
+  *reinterpret_cast<R*>(gx + ((n * g.h + iy) * g.w + ix) * g.c + c0) = Vec<T>::pack(acc);
+}
+
+template <typename T>
+int maxpool(const PoolGeom& g, const void* x, void* y, void* idx, hipStream_t st) {
+  constexpr int V = Vec<T>::N;
+  if (g.c % V || !al16(x) || !al16(y) || ((uintptr_t)idx & (V - 1))) return WAM_ERR_UNSUPPORTED;
+  const int64_t total = g.n * g.ho * g.wo * (g.c / V);
+  hipLaunchKernelGGL(k_maxpool_fwd<T>, (unsigned)((total + kBlk - 1) / kBlk), kBlk, 0, st, g, (const T*)x, (T*)y,
+                     (uint8_t*)idx);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+template <typename T>
+int maxpool_bwd(const PoolGeom& g, const void* gy, const void* idx, void* gx, int relu, hipStream_t st) {
+  constexpr int V = Vec<T>::N;
+  if (g.c % V || !al16(gy) || !al16(gx) || ((uintptr_t)idx & (V - 1))) return WAM_ERR_UNSUPPORTED;
+  const int64_t total = g.n * g.h * g.w * (g.c / V);
+  const unsigned grid = (unsigned)((total + kBlk - 1) / kBlk);
+  if (relu)
+    hipLaunchKernelGGL((k_maxpool_bwd<T, true>), grid, kBlk, 0, st, g, (const T*)gy, (const uint8_t*)idx, (T*)gx);
+  else
+    hipLaunchKernelGGL((k_maxpool_bwd<T, false>), grid, kBlk, 0, st, g, (const T*)gy, (const uint8_t*)idx, (T*)gx);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+inline bool pool_geom(PoolGeom& g, int64_t n, int64_t h, int64_t w, int64_t c, int k, int s, int p) {
+  if (n < 0 || h < 1 || w < 1 || c < 1 || k < 1 || k * k > 127 || s < 1 || p < 0 || 2 * p > k) return false;
+  g.n = n, g.h = h, g.w = w, g.c = c, g.k = k, g.s = s, g.p = p;
+  g.ho = (h + 2 * p - k) / s + 1;
+  g.wo = (w + 2 * p - k) / s + 1;
+  return g.ho >= 1 && g.wo >= 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -299,6 +442,28 @@ int wam_ew_relu_mask(int dtype, int64_t n, const void* g1, const void* g2, const
   if (n == 0) return WAM_OK;
   return dtype == WAM_DT_F32 ? relu_mask<float>(n, g1, g2, y, out, (hipStream_t)stream)
                              : relu_mask<uint16_t>(n, g1, g2, y, out, (hipStream_t)stream);
+}
+
+int wam_ew_maxpool_nhwc(int dtype, int64_t n, int64_t h, int64_t w, int64_t c, int k, int stride, int pad,
+                        const void* x, void* y, void* idx, void* stream) {
+  PoolGeom g;
+  if (!pool_geom(g, n, h, w, c, k, stride, pad) || (n > 0 && (!x || !y || !idx)) ||
+      (dtype != WAM_DT_F32 && dtype != WAM_DT_BF16))
+    return WAM_ERR_INVALID_ARG;
+  if (n == 0) return WAM_OK;
+  return dtype == WAM_DT_F32 ? maxpool<float>(g, x, y, idx, (hipStream_t)stream)
+                             : maxpool<uint16_t>(g, x, y, idx, (hipStream_t)stream);
+}
+
+int wam_ew_maxpool_nhwc_backward(int dtype, int64_t n, int64_t h, int64_t w, int64_t c, int k, int stride, int pad,
+                                 const void* gy, const void* idx, int relu, void* gx, void* stream) {
+  PoolGeom g;
+  if (!pool_geom(g, n, h, w, c, k, stride, pad) || (n > 0 && (!gy || !idx || !gx)) ||
+      (dtype != WAM_DT_F32 && dtype != WAM_DT_BF16))
+    return WAM_ERR_INVALID_ARG;
+  if (n == 0) return WAM_OK;
+  return dtype == WAM_DT_F32 ? maxpool_bwd<float>(g, gy, idx, gx, relu, (hipStream_t)stream)
+                             : maxpool_bwd<uint16_t>(g, gy, idx, gx, relu, (hipStream_t)stream);
 }
 
 }  // extern "C"

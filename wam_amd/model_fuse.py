@@ -93,6 +93,34 @@ def relu_mask(g, y, g2=None):
     return out
 
 
+def _pool_ok(y, k, s, p):
+    v = 8 if y.dtype == torch.bfloat16 else 4
+    return (y.is_cuda and y.dim() == 4 and y.dtype in _DT and y.shape[1] % v == 0 and 2 * p <= k and k * k <= 127
+            and y.is_contiguous(memory_format=torch.channels_last))
+
+
+def maxpool_nhwc(y, k, s, p):
+    """max_pool2d(y, k, s, p) of a channels_last activation -> (out, byte window index)."""
+    n, c, h, w = y.shape
+    ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    out = torch.empty((n, c, ho, wo), dtype=y.dtype, device=y.device, memory_format=torch.channels_last)
+    idx = torch.empty((n, ho, wo, c), dtype=torch.uint8, device=y.device)
+    _lib.check(_lib.lib.wam_ew_maxpool_nhwc(_dt(y), n, h, w, c, k, s, p, _lib.ptr(y), _lib.ptr(out), _lib.ptr(idx),
+                                            _stream(y)))
+    return out, idx
+
+
+def maxpool_nhwc_backward(gy, idx, in_shape, k, s, p, relu):
+    """Input gradient of maxpool_nhwc (channels_last); relu also applies the mask of the ReLU
+    that produced the pooled input."""
+    n, c, h, w = in_shape
+    gy = gy.contiguous(memory_format=torch.channels_last)
+    gx = torch.empty((n, c, h, w), dtype=gy.dtype, device=gy.device, memory_format=torch.channels_last)
+    _lib.check(_lib.lib.wam_ew_maxpool_nhwc_backward(_dt(gy), n, h, w, c, k, s, p, _lib.ptr(gy), _lib.ptr(idx),
+                                                     int(relu), _lib.ptr(gx), _stream(gy)))
+    return gx
+
+
 def _conv_nd(x, w, stride, padding, dilation, groups):
     return torch.ops.aten.convolution(x, w, None, stride, padding, dilation, False, [0] * len(stride), groups)
 
@@ -253,6 +281,43 @@ class _PolyphaseReLUFn(torch.autograd.Function):
         return _PolyphaseInputGrad.backward(_C, gm)
 
 
+class _PolyphaseReLUPoolFn(torch.autograd.Function):
+    """maxpool(relu(InputConv2d(x))): the pooled input is not kept -- the byte window index
+    carries the ReLU mask, so the backward is one gather kernel + the polyphase convolution."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, wpoly, pad, geom, pool):
+        y = bias_act_(F.conv2d(x, weight, None, 2, pad), bias, True)
+        k, s, p = pool
+        ctx.geom, ctx.in_hw, ctx.pool, ctx.y_shape = geom, x.shape[-2:], pool, y.shape
+        if _pool_ok(y, k, s, p):
+            out, idx = maxpool_nhwc(y, k, s, p)
+            ctx.save_for_backward(wpoly, idx)
+            ctx.hip = True
+        else:
+            out, idx = F.max_pool2d(y, k, s, p, return_indices=True)
+            ctx.save_for_backward(wpoly, idx, y)
+            ctx.hip = False
+        return out
+
+    @staticmethod
+    def backward(ctx, go):
+        k, s, p = ctx.pool
+        if ctx.hip:
+            wpoly, idx = ctx.saved_tensors
+            gm = maxpool_nhwc_backward(go, idx, ctx.y_shape, k, s, p, relu=True)
+        else:
+            wpoly, idx, y = ctx.saved_tensors
+            gy = torch.ops.aten.max_pool2d_with_indices_backward(go, y, [k, k], [s, s], [p, p], [1, 1], False, idx)
+            gm = relu_mask(gy, y)
+
+        class _C:  # reuse the polyphase backward with its saved table
+            saved_tensors = (wpoly,)
+            geom = ctx.geom
+            in_hw = ctx.in_hw
+        return _PolyphaseInputGrad.backward(_C, gm) + (None,)
+
+
 def _geom(conv):
     return (list(conv.stride), list(conv.padding), list(conv.dilation), conv.groups)
 
@@ -327,6 +392,40 @@ class InputConvReLU(nn.Module):
         b = ic.bias if ic.bias is not None else torch.zeros(ic.weight.shape[0], dtype=ic.weight.dtype,
                                                             device=ic.weight.device)
         return _PolyphaseReLUFn.apply(x, ic.weight, b, ic.wpoly, ic.pad, ((oy, Ty, ny), (ox, Tx, nx)))
+
+
+class InputConvReLUPool(InputConvReLU):
+    """maxpool(relu(InputConv2d(x))) for a square, undilated, floor-mode max pool."""
+
+    def __init__(self, ic, pool):
+        super().__init__(ic)
+        self.pool = pool  # (k, stride, pad)
+
+    def forward(self, x):
+        from .model_opt import _phase_geometry
+        ic = self.ic
+        H, W = x.shape[-2:]
+        oy, Ty, _, ny = _phase_geometry(ic.kh, ic.pad[0], H)
+        ox, Tx, _, nx = _phase_geometry(ic.kw, ic.pad[1], W)
+        b = ic.bias if ic.bias is not None else torch.zeros(ic.weight.shape[0], dtype=ic.weight.dtype,
+                                                            device=ic.weight.device)
+        return _PolyphaseReLUPoolFn.apply(x, ic.weight, b, ic.wpoly, ic.pad, ((oy, Ty, ny), (ox, Tx, nx)), self.pool)
+
+
+def _square(v):
+    if isinstance(v, (tuple, list)):
+        return v[0] if len(set(v)) == 1 else None
+    return v
+
+
+def _simple_pool(m):
+    """(k, stride, pad) of a MaxPool2d the fused kernels implement, or None."""
+    if type(m) is not nn.MaxPool2d or m.ceil_mode or m.return_indices or _square(m.dilation) != 1:
+        return None
+    k, s, p = _square(m.kernel_size), _square(m.stride if m.stride is not None else m.kernel_size), _square(m.padding)
+    if None in (k, s, p) or 2 * p > k or k * k > 127:
+        return None
+    return (int(k), int(s), int(p))
 
 
 # --------------------------------------------------------------------------------- graph rewrite
@@ -416,6 +515,20 @@ def fuse_elementwise(gm):
             for a in drop:
                 g.erase_node(a)
             count += 1
+    for node in list(g.nodes):  # stem relu -> max pool
+        if node.op != "call_module" or _simple_pool(mods.get(node.target)) is None:
+            continue
+        src = node.args[0] if node.args else None
+        if not isinstance(src, fx.Node) or src.op != "call_module" or len(src.users) != 1 \
+                or type(mods.get(src.target)) is not InputConvReLU:
+            continue
+        name = add_mod(src.target, InputConvReLUPool(mods[src.target].ic, _simple_pool(mods[node.target])))
+        with g.inserting_before(node):
+            new = g.call_module(name, (src.args[0],))
+        node.replace_all_uses_with(new)
+        g.erase_node(node)
+        g.erase_node(src)
+        count += 1
     _link_skip_gradients(gm, mods)
     g.lint()
     gm.recompile()
