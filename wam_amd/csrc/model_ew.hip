@@ -291,16 +291,17 @@ __global__ void __launch_bounds__(kBlk) k_maxpool_fwd(PoolGeom g, const T* __res
                                                         uint8_t* __restrict__ idx) {
   constexpr int V = Vec<T>::N;
   typedef typename Vec<T>::raw R;
-  const int64_t cv = g.c / V;
-  const int64_t total = g.n * g.ho * g.wo * cv;
-  const int64_t q = (int64_t)blockIdx.x * kBlk + threadIdx.x;
+  // 32-bit index decomposition (the host checks total < 2^31): 64-bit divides are ~100 VALU ops
+  const uint32_t cv = (uint32_t)(g.c / V);
+  const uint32_t total = (uint32_t)(g.n * g.ho * g.wo) * cv;
+  const uint32_t q = blockIdx.x * kBlk + threadIdx.x;
   if (q >= total) return;
-  int64_t r = q / cv;
-  const int64_t c0 = (q - r * cv) * V;
-  const int64_t ox = r % g.wo;
-  r /= g.wo;
-  const int64_t oy = r % g.ho;
-  const int64_t n = r / g.ho;
+  uint32_t r = q / cv;
+  const int64_t c0 = (int64_t)(q - r * cv) * V;
+  const int64_t ox = r % (uint32_t)g.wo;
+  r /= (uint32_t)g.wo;
+  const int64_t oy = r % (uint32_t)g.ho;
+  const int64_t n = r / (uint32_t)g.ho;
   const int64_t y0 = oy * g.s - g.p, x0 = ox * g.s - g.p;
   const int ky0 = (int)max<int64_t>(0, -y0), ky1 = (int)min<int64_t>(g.k, g.h - y0);
   const int kx0 = (int)max<int64_t>(0, -x0), kx1 = (int)min<int64_t>(g.k, g.w - x0);
@@ -338,26 +339,28 @@ __global__ void __launch_bounds__(kBlk) k_maxpool_bwd(PoolGeom g, const T* __res
                                                         const uint8_t* __restrict__ idx, T* __restrict__ gx) {
   constexpr int V = Vec<T>::N;
   typedef typename Vec<T>::raw R;
-  const int64_t cv = g.c / V;
-  const int64_t total = g.n * g.h * g.w * cv;
-  const int64_t q = (int64_t)blockIdx.x * kBlk + threadIdx.x;
+  const uint32_t cv = (uint32_t)(g.c / V);
+  const uint32_t total = (uint32_t)(g.n * g.h * g.w) * cv;
+  const uint32_t q = blockIdx.x * kBlk + threadIdx.x;
   if (q >= total) return;
-  int64_t r = q / cv;
-  const int64_t c0 = (q - r * cv) * V;
-  const int64_t ix = r % g.w;
-  r /= g.w;
-  const int64_t iy = r % g.h;
-  const int64_t n = r / g.h;
-  // windows oy with oy*s - p <= iy <= oy*s - p + k - 1
-  const int64_t oy0 = max<int64_t>(0, (iy + g.p - g.k + g.s) / g.s), oy1 = min<int64_t>(g.ho - 1, (iy + g.p) / g.s);
-  const int64_t ox0 = max<int64_t>(0, (ix + g.p - g.k + g.s) / g.s), ox1 = min<int64_t>(g.wo - 1, (ix + g.p) / g.s);
+  uint32_t r = q / cv;
+  const int64_t c0 = (int64_t)(q - r * cv) * V;
+  const int ix = (int)(r % (uint32_t)g.w);
+  r /= (uint32_t)g.w;
+  const int iy = (int)(r % (uint32_t)g.h);
+  const int64_t n = r / (uint32_t)g.h;
+  // windows oy with oy*s - p <= iy <= oy*s - p + k - 1 (32-bit: a negative numerator truncates
+  // toward zero, which the max with 0 absorbs)
+  const int ho = (int)g.ho, wo = (int)g.wo;
+  const int oy0 = max(0, (iy + g.p - g.k + g.s) / g.s), oy1 = min(ho - 1, (iy + g.p) / g.s);
+  const int ox0 = max(0, (ix + g.p - g.k + g.s) / g.s), ox1 = min(wo - 1, (ix + g.p) / g.s);
   float acc[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) acc[j] = 0.f;
-  for (int64_t oy = oy0; oy <= oy1; ++oy) {
-    const int py = (int)(iy - (oy * g.s - g.p));
-    for (int64_t ox = ox0; ox <= ox1; ++ox) {
-      const int pos = py * g.k + (int)(ix - (ox * g.s - g.p));
+  for (int oy = oy0; oy <= oy1; ++oy) {
+    const int py = iy - (oy * g.s - g.p);
+    for (int ox = ox0; ox <= ox1; ++ox) {
+      const int pos = py * g.k + (ix - (ox * g.s - g.p));
       const int64_t o = ((n * g.ho + oy) * g.wo + ox) * g.c + c0;
       float v[V];
       Vec<T>::unpack(*reinterpret_cast<const R*>(gy + o), v);
@@ -384,6 +387,7 @@ int maxpool(const PoolGeom& g, const void* x, void* y, void* idx, hipStream_t st
   constexpr int V = Vec<T>::N;
   if (g.c % V || !al16(x) || !al16(y) || ((uintptr_t)idx & (V - 1))) return WAM_ERR_UNSUPPORTED;
   const int64_t total = g.n * g.ho * g.wo * (g.c / V);
+  if (total >= (int64_t(1) << 31) - kBlk) return WAM_ERR_UNSUPPORTED;
   hipLaunchKernelGGL(k_maxpool_fwd<T>, (unsigned)((total + kBlk - 1) / kBlk), kBlk, 0, st, g, (const T*)x, (T*)y,
                      (uint8_t*)idx);
   WAM_LAUNCH_CHECK();
@@ -395,6 +399,7 @@ int maxpool_bwd(const PoolGeom& g, const void* gy, const void* idx, void* gx, in
   constexpr int V = Vec<T>::N;
   if (g.c % V || !al16(gy) || !al16(gx) || ((uintptr_t)idx & (V - 1))) return WAM_ERR_UNSUPPORTED;
   const int64_t total = g.n * g.h * g.w * (g.c / V);
+  if (total >= (int64_t(1) << 31) - kBlk || g.h >= (1 << 30) || g.w >= (1 << 30)) return WAM_ERR_UNSUPPORTED;
   const unsigned grid = (unsigned)((total + kBlk - 1) / kBlk);
   if (relu)
     hipLaunchKernelGGL((k_maxpool_bwd<T, true>), grid, kBlk, 0, st, g, (const T*)gy, (const uint8_t*)idx, (T*)gx);
