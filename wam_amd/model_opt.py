@@ -87,8 +87,16 @@ class _PolyphaseInputGrad(torch.autograd.Function):
         py0, px0 = -oy, -ox
         py1 = (ny - 1 + oy + Ty - 1) - (go.shape[-2] - 1)
         px1 = (nx - 1 + ox + Tx - 1) - (go.shape[-1] - 1)
-        gp = F.pad(go, (px0, px1, py0, py1))
-        gx = F.pixel_shuffle(F.conv2d(gp, wpoly.to(go.dtype)), 2)
+        if min(py0, py1, px0, px1) >= 0:
+            # the convolution's own (symmetric) zero padding and a crop of the surplus rows /
+            # columns instead of an F.pad copy: 5.8 -> 4.3 ms per c2 model call, bit-identical
+            # (scripts/stem_probe.py)
+            P, Q = max(py0, py1), max(px0, px1)
+            go_ = F.conv2d(go, wpoly.to(go.dtype), padding=(P, Q))
+            go_ = go_[..., P - py0:P - py0 + ny, Q - px0:Q - px0 + nx]
+        else:
+            go_ = F.conv2d(F.pad(go, (px0, px1, py0, py1)), wpoly.to(go.dtype))
+        gx = F.pixel_shuffle(go_, 2)
         return gx[..., :H, :W], None, None, None, None, None
 
 
