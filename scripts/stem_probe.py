@@ -1,7 +1,8 @@
 """Stem input-gradient variants at the c2 model batch (832 x 64 x 112 x 112 bf16, channels_last):
 (a) polyphase with an explicit F.pad (model_opt._PolyphaseInputGrad), (b) polyphase with the
 conv's own symmetric padding and a crop, (c) as (b) with the gradient in NCHW, (d) MIOpen
-backward-data of the original 7x7/2 convolution. Times (median of 7) and max |diff| vs (a)."""
+backward-data of the original 7x7/2 convolution, (e-g) as (b) with the 12 output channels
+zero-padded to 16/32/64. Times (median of 7) and max |diff| vs (a)."""
 import os
 import sys
 import time
@@ -64,9 +65,20 @@ def main(batch=832):
         return torch.ops.aten.convolution_backward(go, x, conv.weight, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
                                                    [True, False, False])[0]
 
+    def padded(cout):
+        wp = torch.zeros(cout, *ic.wpoly.shape[1:], dtype=ic.wpoly.dtype, device="cuda")
+        wp[:ic.wpoly.shape[0]] = ic.wpoly
+
+        def e():
+            o = F.conv2d(go, wp, padding=(P, Q))
+            o = o[:, :ic.wpoly.shape[0], P - py0:P - py0 + ny, Q - px0:Q - px0 + nx]
+            return F.pixel_shuffle(o, 2)[..., :H, :W]
+        return e
+
     ref = a().float()
     print("pads", (py0, py1, px0, px1))
-    for name, fn in (("a pad+polyphase", a), ("b conv-pad+crop", b), ("c conv-pad NCHW", c), ("d miopen bwd-data", d)):
+    for name, fn in (("a pad+polyphase", a), ("b conv-pad+crop", b), ("c conv-pad NCHW", c), ("d miopen bwd-data", d),
+                     ("e b, 16 out ch", padded(16)), ("f b, 32 out ch", padded(32)), ("g b, 64 out ch", padded(64))):
         t = timeit(fn)
         diff = (fn().float() - ref).abs().max().item()
         print("%-18s %8.3f ms  max|diff vs a| %.3e" % (name, t, diff))
