@@ -284,24 +284,27 @@ int relu_mask(int64_t n, const void* g1_, const void* g2_, const void* y_, void*
 struct PoolGeom {
   int64_t n, h, w, c, ho, wo;
   int k, s, p;
+  int cv, cv_sh, s_sh;  // channel vectors per pixel; log2 of cv / s when a power of two, else -1
 };
 
-template <typename T>
+// a / d through a shift when d is a power of two (floor division; callers clamp negatives to 0)
+__device__ __forceinline__ int div_sh(int a, int sh, int d) { return sh >= 0 ? (a >> sh) : a / d; }
+
+// KC: compile-time window size (3 for the ResNet stem; 0 = runtime g.k). With KC all k*k loads
+// are issued at once from clamped addresses and masked afterwards, instead of a loop of dependent
+// load rounds (the kernel is latency-bound otherwise).
+template <typename T, int KC>
 __global__ void __launch_bounds__(kBlk) k_maxpool_fwd(PoolGeom g, const T* __restrict__ x, T* __restrict__ y,
                                                         uint8_t* __restrict__ idx) {
   constexpr int V = Vec<T>::N;
   typedef typename Vec<T>::raw R;
-  // 32-bit index decomposition (the host checks total < 2^31): 64-bit divides are ~100 VALU ops
-  const uint32_t cv = (uint32_t)(g.c / V);
-  const uint32_t total = (uint32_t)(g.n * g.ho * g.wo) * cv;
-  const uint32_t q = blockIdx.x * kBlk + threadIdx.x;
-  if (q >= total) return;
-  uint32_t r = q / cv;
-  const int64_t c0 = (int64_t)(q - r * cv) * V;
-  const int64_t ox = r % (uint32_t)g.wo;
-  r /= (uint32_t)g.wo;
-  const int64_t oy = r % (uint32_t)g.ho;
-  const int64_t n = r / (uint32_t)g.ho;
+  // grid (x: output column x channel vector, y: output row, z: image): no 64-bit divides, which
+  // cost ~100 VALU ops each and made the first version issue-bound
+  const int t = blockIdx.x * kBlk + threadIdx.x;
+  const int ox = div_sh(t, g.cv_sh, g.cv);
+  if (ox >= g.wo) return;
+  const int64_t c0 = (int64_t)(t - ox * g.cv) * V;
+  const int64_t oy = blockIdx.y, n = blockIdx.z;
   const int64_t y0 = oy * g.s - g.p, x0 = ox * g.s - g.p;
   const int ky0 = (int)max<int64_t>(0, -y0), ky1 = (int)min<int64_t>(g.k, g.h - y0);
   const int kx0 = (int)max<int64_t>(0, -x0), kx1 = (int)min<int64_t>(g.k, g.w - x0);
@@ -309,14 +312,38 @@ __global__ void __launch_bounds__(kBlk) k_maxpool_fwd(PoolGeom g, const T* __res
   int id[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) m[j] = -INFINITY, id[j] = ky0 * g.k + kx0;
-  for (int ky = ky0; ky < ky1; ++ky) {
-    const T* row = x + ((n * g.h + y0 + ky) * g.w) * g.c + c0;
-    for (int kx = kx0; kx < kx1; ++kx) {
-      float v[V];
-      Vec<T>::unpack(*reinterpret_cast<const R*>(row + (x0 + kx) * g.c), v);
+  if constexpr (KC > 0) {
+    R raw[KC * KC];
 #pragma unroll
-      for (int j = 0; j < V; ++j)
-        if (v[j] > m[j] || isnan(v[j])) m[j] = v[j], id[j] = ky * g.k + kx;
+    for (int ky = 0; ky < KC; ++ky) {
+      const int64_t yy = min<int64_t>(max<int64_t>(y0 + ky, 0), g.h - 1);
+#pragma unroll
+      for (int kx = 0; kx < KC; ++kx) {
+        const int64_t xx = min<int64_t>(max<int64_t>(x0 + kx, 0), g.w - 1);
+        raw[ky * KC + kx] = *reinterpret_cast<const R*>(x + ((n * g.h + yy) * g.w + xx) * g.c + c0);
+      }
+    }
+#pragma unroll
+    for (int ky = 0; ky < KC; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < KC; ++kx) {
+        if (ky < ky0 || ky >= ky1 || kx < kx0 || kx >= kx1) continue;
+        float v[V];
+        Vec<T>::unpack(raw[ky * KC + kx], v);
+#pragma unroll
+        for (int j = 0; j < V; ++j)
+          if (v[j] > m[j] || isnan(v[j])) m[j] = v[j], id[j] = ky * KC + kx;
+      }
+  } else {
+    for (int ky = ky0; ky < ky1; ++ky) {
+      const T* row = x + ((n * g.h + y0 + ky) * g.w) * g.c + c0;
+      for (int kx = kx0; kx < kx1; ++kx) {
+        float v[V];
+        Vec<T>::unpack(*reinterpret_cast<const R*>(row + (x0 + kx) * g.c), v);
+#pragma unroll
+        for (int j = 0; j < V; ++j)
+          if (v[j] > m[j] || isnan(v[j])) m[j] = v[j], id[j] = ky * g.k + kx;
+      }
     }
   }
   const int64_t o = ((n * g.ho + oy) * g.wo + ox) * g.c + c0;
@@ -334,62 +361,113 @@ __global__ void __launch_bounds__(kBlk) k_maxpool_fwd(PoolGeom g, const T* __res
   }
 }
 
-template <typename T, bool RELU>
+// W2: at most 2 windows per axis cover a pixel (ceil(k / s) <= 2, e.g. 3x3 stride 2): the four
+// candidate (gradient, index) pairs are loaded at once from clamped addresses, then summed in
+// the loop's (oy, ox) order.
+template <typename T, bool RELU, bool W2>
 __global__ void __launch_bounds__(kBlk) k_maxpool_bwd(PoolGeom g, const T* __restrict__ gy,
                                                         const uint8_t* __restrict__ idx, T* __restrict__ gx) {
   constexpr int V = Vec<T>::N;
   typedef typename Vec<T>::raw R;
-  const uint32_t cv = (uint32_t)(g.c / V);
-  const uint32_t total = (uint32_t)(g.n * g.h * g.w) * cv;
-  const uint32_t q = blockIdx.x * kBlk + threadIdx.x;
-  if (q >= total) return;
-  uint32_t r = q / cv;
-  const int64_t c0 = (int64_t)(q - r * cv) * V;
-  const int ix = (int)(r % (uint32_t)g.w);
-  r /= (uint32_t)g.w;
-  const int iy = (int)(r % (uint32_t)g.h);
-  const int64_t n = r / (uint32_t)g.h;
-  // windows oy with oy*s - p <= iy <= oy*s - p + k - 1 (32-bit: a negative numerator truncates
-  // toward zero, which the max with 0 absorbs)
+  const int t = blockIdx.x * kBlk + threadIdx.x;
+  const int ix = div_sh(t, g.cv_sh, g.cv);
+  if (ix >= g.w) return;
+  const int64_t c0 = (int64_t)(t - ix * g.cv) * V;
+  const int iy = blockIdx.y;
+  const int64_t n = blockIdx.z;
+  // windows oy with oy*s - p <= iy <= oy*s - p + k - 1
   const int ho = (int)g.ho, wo = (int)g.wo;
-  const int oy0 = max(0, (iy + g.p - g.k + g.s) / g.s), oy1 = min(ho - 1, (iy + g.p) / g.s);
-  const int ox0 = max(0, (ix + g.p - g.k + g.s) / g.s), ox1 = min(wo - 1, (ix + g.p) / g.s);
+  const int oy0 = max(0, div_sh(iy + g.p - g.k + g.s, g.s_sh, g.s)), oy1 = min(ho - 1, div_sh(iy + g.p, g.s_sh, g.s));
+  const int ox0 = max(0, div_sh(ix + g.p - g.k + g.s, g.s_sh, g.s)), ox1 = min(wo - 1, div_sh(ix + g.p, g.s_sh, g.s));
   float acc[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) acc[j] = 0.f;
-  for (int oy = oy0; oy <= oy1; ++oy) {
-    const int py = iy - (oy * g.s - g.p);
-    for (int ox = ox0; ox <= ox1; ++ox) {
-      const int pos = py * g.k + (ix - (ox * g.s - g.p));
-      const int64_t o = ((n * g.ho + oy) * g.wo + ox) * g.c + c0;
-      float v[V];
-      Vec<T>::unpack(*reinterpret_cast<const R*>(gy + o), v);
-      uint8_t b[V];
-      if constexpr (V == 8) {
-        const uint2 w = *reinterpret_cast<const uint2*>(idx + o);
+  auto unpack_idx = [&](const uint8_t* ip, uint8_t (&b)[V]) {
+    if constexpr (V == 8) {
+      const uint2 w = *reinterpret_cast<const uint2*>(ip);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = (uint8_t)(w.x >> (8 * j)), b[4 + j] = (uint8_t)(w.y >> (8 * j));
-      } else {
-        const uint32_t w = *reinterpret_cast<const uint32_t*>(idx + o);
+      for (int j = 0; j < 4; ++j) b[j] = (uint8_t)(w.x >> (8 * j)), b[4 + j] = (uint8_t)(w.y >> (8 * j));
+    } else {
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(ip);
 #pragma unroll
-        for (int j = 0; j < V; ++j) b[j] = (uint8_t)(w >> (8 * j));
+      for (int j = 0; j < V; ++j) b[j] = (uint8_t)(w >> (8 * j));
+    }
+  };
+  auto add = [&](const float (&v)[V], const uint8_t (&b)[V], int pos) {
+#pragma unroll
+    for (int j = 0; j < V; ++j)
+      if ((b[j] & 0x7f) == pos && (!RELU || (b[j] & 0x80))) acc[j] += v[j];
+  };
+  if constexpr (W2) {
+    R rg[4];
+    uint8_t rb[4][V];
+    int wy[2], wx[2];
+    bool ok[4];
+    wy[0] = min(oy0, ho - 1), wy[1] = min(oy0 + 1, ho - 1);
+    wx[0] = min(ox0, wo - 1), wx[1] = min(ox0 + 1, wo - 1);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int64_t o = ((n * g.ho + wy[a]) * g.wo + wx[b]) * g.c + c0;
+        rg[2 * a + b] = *reinterpret_cast<const R*>(gy + o);
+        unpack_idx(idx + o, rb[2 * a + b]);
+        ok[2 * a + b] = oy0 + a <= oy1 && ox0 + b <= ox1;
       }
 #pragma unroll
-      for (int j = 0; j < V; ++j)
-        if ((b[j] & 0x7f) == pos && (!RELU || (b[j] & 0x80))) acc[j] += v[j];
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        if (!ok[2 * a + b]) continue;
+        const int pos = (iy - ((oy0 + a) * g.s - g.p)) * g.k + (ix - ((ox0 + b) * g.s - g.p));
+        float v[V];
+        Vec<T>::unpack(rg[2 * a + b], v);
+        add(v, rb[2 * a + b], pos);
+      }
+  } else {
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      const int py = iy - (oy * g.s - g.p);
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const int pos = py * g.k + (ix - (ox * g.s - g.p));
+        const int64_t o = ((n * g.ho + oy) * g.wo + ox) * g.c + c0;
+        float v[V];
+        Vec<T>::unpack(*reinterpret_cast<const R*>(gy + o), v);
+        uint8_t b[V];
+        unpack_idx(idx + o, b);
+        add(v, b, pos);
+      }
     }
   }
   *reinterpret_cast<R*>(gx + ((n * g.h + iy) * g.w + ix) * g.c + c0) = Vec<T>::pack(acc);
+}
+
+inline int log2_exact(int64_t d) {
+  for (int b = 0; b < 31; ++b)
+    if ((int64_t(1) << b) == d) return b;
+  return -1;
+}
+
+// fill the launch-side fields; false when a grid dimension or a 32-bit index would overflow
+inline bool pool_grid(PoolGeom& g, int V) {
+  g.cv = (int)(g.c / V);
+  g.cv_sh = (int)log2_exact(g.cv);
+  g.s_sh = (int)log2_exact(g.s);
+  const int64_t lim = 65535;
+  return g.n <= lim && g.h <= lim && g.ho <= lim && g.w * g.cv < (int64_t(1) << 30) &&
+         g.n * g.h * g.w * g.c < (int64_t(1) << 62);
 }
 
 template <typename T>
 int maxpool(const PoolGeom& g, const void* x, void* y, void* idx, hipStream_t st) {
   constexpr int V = Vec<T>::N;
   if (g.c % V || !al16(x) || !al16(y) || ((uintptr_t)idx & (V - 1))) return WAM_ERR_UNSUPPORTED;
-  const int64_t total = g.n * g.ho * g.wo * (g.c / V);
-  if (total >= (int64_t(1) << 31) - kBlk) return WAM_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL(k_maxpool_fwd<T>, (unsigned)((total + kBlk - 1) / kBlk), kBlk, 0, st, g, (const T*)x, (T*)y,
-                     (uint8_t*)idx);
+  PoolGeom gg = g;
+  if (!pool_grid(gg, V)) return WAM_ERR_UNSUPPORTED;
+  const dim3 grid((unsigned)((gg.wo * gg.cv + kBlk - 1) / kBlk), (unsigned)gg.ho, (unsigned)gg.n);
+  if (gg.k == 3)
+    hipLaunchKernelGGL((k_maxpool_fwd<T, 3>), grid, kBlk, 0, st, gg, (const T*)x, (T*)y, (uint8_t*)idx);
+  else
+    hipLaunchKernelGGL((k_maxpool_fwd<T, 0>), grid, kBlk, 0, st, gg, (const T*)x, (T*)y, (uint8_t*)idx);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }
@@ -398,13 +476,16 @@ template <typename T>
 int maxpool_bwd(const PoolGeom& g, const void* gy, const void* idx, void* gx, int relu, hipStream_t st) {
   constexpr int V = Vec<T>::N;
   if (g.c % V || !al16(gy) || !al16(gx) || ((uintptr_t)idx & (V - 1))) return WAM_ERR_UNSUPPORTED;
-  const int64_t total = g.n * g.h * g.w * (g.c / V);
-  if (total >= (int64_t(1) << 31) - kBlk || g.h >= (1 << 30) || g.w >= (1 << 30)) return WAM_ERR_UNSUPPORTED;
-  const unsigned grid = (unsigned)((total + kBlk - 1) / kBlk);
-  if (relu)
-    hipLaunchKernelGGL((k_maxpool_bwd<T, true>), grid, kBlk, 0, st, g, (const T*)gy, (const uint8_t*)idx, (T*)gx);
-  else
-    hipLaunchKernelGGL((k_maxpool_bwd<T, false>), grid, kBlk, 0, st, g, (const T*)gy, (const uint8_t*)idx, (T*)gx);
+  PoolGeom gg = g;
+  if (!pool_grid(gg, V)) return WAM_ERR_UNSUPPORTED;
+  const dim3 grid((unsigned)((gg.w * gg.cv + kBlk - 1) / kBlk), (unsigned)gg.h, (unsigned)gg.n);
+  const bool w2 = (gg.k + gg.s - 1) / gg.s <= 2;
+  const T* gyp = (const T*)gy;
+  const uint8_t* ip = (const uint8_t*)idx;
+  if (relu && w2) hipLaunchKernelGGL((k_maxpool_bwd<T, true, true>), grid, kBlk, 0, st, gg, gyp, ip, (T*)gx);
+  else if (relu) hipLaunchKernelGGL((k_maxpool_bwd<T, true, false>), grid, kBlk, 0, st, gg, gyp, ip, (T*)gx);
+  else if (w2) hipLaunchKernelGGL((k_maxpool_bwd<T, false, true>), grid, kBlk, 0, st, gg, gyp, ip, (T*)gx);
+  else hipLaunchKernelGGL((k_maxpool_bwd<T, false, false>), grid, kBlk, 0, st, gg, gyp, ip, (T*)gx);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }

@@ -96,7 +96,8 @@ def relu_mask(g, y, g2=None):
 def _pool_ok(y, k, s, p):
     v = 8 if y.dtype == torch.bfloat16 else 4
     return (y.is_cuda and y.dim() == 4 and y.dtype in _DT and y.shape[1] % v == 0 and 2 * p <= k and k * k <= 127
-            and y.is_contiguous(memory_format=torch.channels_last) and y.numel() // v < 2 ** 31 - 256)
+            and y.is_contiguous(memory_format=torch.channels_last) and y.shape[0] <= 65535 and y.shape[2] <= 65535
+            and y.shape[3] * (y.shape[1] // v) < 2 ** 30)
 
 
 def maxpool_nhwc(y, k, s, p):
