@@ -179,8 +179,23 @@ __global__ void __launch_bounds__(256) k_frame_accumulate(int64_t groups, int64_
     if (sidx < 0) continue;
     const int32_t b = band[p];
     double acc = frame[t];
-    for (int64_t s = 0; s < groups; ++s) {
-      float v = maps[(s * group_items + n) * maps_item_len + sidx];
+    // samples in blocks of 8: the block's loads are issued together, the fp64 sum stays in
+    // sample order (the reference accumulates sample by sample)
+    const float* mp = maps + n * maps_item_len + sidx;
+    const int64_t mstride = group_items * maps_item_len;
+    int64_t s = 0;
+    for (; s + 8 <= groups; s += 8) {
+      float v[8], m[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[u] = mp[(s + u) * mstride];
+        m[u] = normalize ? band_max[(s + u) * n_bands + b] : 1.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += (double)(normalize ? v[u] / m[u] : v[u]);
+    }
+    for (; s < groups; ++s) {
+      float v = mp[s * mstride];
       if (normalize) v = v / band_max[s * n_bands + b];
       acc += (double)v;
     }
