@@ -220,15 +220,15 @@ __global__ void __launch_bounds__(256) k_frame_trapz(int64_t groups, int64_t k0,
     const int64_t p = t % frame_len;
     const int64_t n = t / frame_len;
     const int32_t sidx = src[p];
-    const int32_t b = band[p];
+    const int32_t b = sidx >= 0 ? band[p] : 0;  // pixels outside the mosaic load a valid dummy
     float a = acc[t];
     float pv = prev[t];
-    for (int64_t s = 0; s < groups; ++s) {
-      float v = 0.f;
-      if (sidx >= 0) {
-        v = maps[(s * group_items + n) * maps_item_len + sidx];
-        if (normalize) v = v / band_max[s * n_bands + b];
-      }
+    // loads in blocks of 8 steps (issued together), the trapezoid / weighted sum in step order
+    const float* mp = maps + n * maps_item_len + (sidx >= 0 ? sidx : 0);
+    const int64_t mstride = group_items * maps_item_len;
+    auto step = [&](int64_t s, float v, float m) {
+      if (sidx < 0) v = 0.f;
+      else if (normalize) v = v / m;
       v = nan_to_num(v);
       if (weights) {
         a = fmaf(weights[s], v, a);
@@ -236,7 +236,19 @@ __global__ void __launch_bounds__(256) k_frame_trapz(int64_t groups, int64_t k0,
         if (k0 + s > 0) a = a + (pv + v) / 2.0f;
         pv = v;
       }
+    };
+    int64_t s = 0;
+    for (; s + 8 <= groups; s += 8) {
+      float v[8], m[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[u] = mp[(s + u) * mstride];
+        m[u] = normalize ? band_max[(s + u) * n_bands + b] : 1.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) step(s + u, v[u], m[u]);
     }
+    for (; s < groups; ++s) step(s, mp[s * mstride], normalize ? band_max[s * n_bands + b] : 1.f);
     acc[t] = a;
     prev[t] = pv;
   }
