@@ -91,8 +91,22 @@ def test_seed_gradient_matches_autograd_of_reference_loss(y, n):
     out = torch.randn(groups * n, 10, requires_grad=True)
     loss = sum(torch.diag(out[s * n:(s + 1) * n][:, y]).mean() for s in range(groups))
     (g_ref,) = torch.autograd.grad(loss, out)
-    g = engine.seed_gradient(out.detach(), y, groups, n)
-    assert torch.equal(g, g_ref)
+    g, scale = engine.seed_gradient(out.detach(), y, groups, n)
+    assert scale is None and torch.equal(g, g_ref)
+    # unit seed + fp32 scale (the bf16-model form): same gradient, the scale applied afterwards
+    gu, scale = engine.seed_gradient(out.detach(), y, groups, n, unit=True)
+    assert set(gu.unique().tolist()) <= {0.0, 1.0}
+    assert torch.equal(gu * scale, g_ref)
+
+
+def test_input_gradient_bf16_scale_not_rounded():
+    """The 1/N^2 loss scale is applied in fp32 after a bf16 backward (1/9 is not a bf16 value)."""
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(4, 5).to(torch.bfloat16)
+    img = torch.randn(3, 4)
+    g = engine.input_gradient(lambda t: lin(t.to(torch.bfloat16)), img, 2, 1, 3)
+    want = lin.weight[2].float() * float(torch.tensor(1.0) / 9)
+    assert torch.equal(g, want.expand(3, 4).contiguous())
 
 
 def test_legacy_noise_stream_matches_reference_loop():

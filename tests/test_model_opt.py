@@ -131,6 +131,64 @@ def test_fuse_rewrite_structure():
     assert sum(getattr(m, "link_in", None) is not None for m in gm18.modules()) == 4
 
 
+class _AuxBranchNet(nn.Module):
+    """Non-ResNet topology: the producer's output feeds the consumer add's skip operand AND an
+    auxiliary head that does not lead to the add's other operand, plus a broadcast add."""
+
+    def __init__(self):
+        super().__init__()
+        self.c0 = nn.Conv2d(3, 8, 3, padding=1)
+        self.c1 = nn.Conv2d(8, 8, 3, padding=1)
+        self.c2 = nn.Conv2d(8, 8, 3, padding=1)
+        self.pos = nn.Parameter(torch.randn(1, 8, 1, 1))
+        self.aux = nn.Conv2d(8, 8, 1)
+        self.fc = nn.Linear(8, 4)
+
+    def forward(self, x):
+        h = self.c0(x)
+        p = torch.relu(self.c1(h) + h)      # producer (residual add + ReLU)
+        aux = self.aux(p)                   # side branch: never reaches c2(h)
+        q = torch.relu(self.c2(h) + p)      # consumer: a = c2(h), skip operand s = p
+        r = torch.relu(q + self.pos)        # broadcast operand [1, C, 1, 1]
+        return self.fc((r + aux).mean((2, 3)))
+
+
+def test_fuse_guards_non_resnet_patterns():
+    """no skip-gradient link when the producer's other user does not reach the
+    consumer's `a` operand; a broadcast residual add falls back to torch (same values)."""
+    from wam_amd import model_fuse
+    torch.manual_seed(0)
+    gm, _ = model_fuse.fuse_elementwise(torch.fx.symbolic_trace(_AuxBranchNet().eval()))
+    kinds = [type(m).__name__ for m in gm.modules()]
+    assert kinds.count("AddBiasReLU") == 3
+    assert sum(getattr(m, "link_in", None) is not None for m in gm.modules()) == 0
+    assert sum(getattr(m, "link_out", None) is not None for m in gm.modules()) == 0
+    # broadcast / mismatched operands take the torch path (and CPU tensors are never fused)
+    abr = model_fuse.AddBiasReLU(torch.randn(8), None)
+    a, s = torch.randn(2, 8, 4, 4), torch.randn(1, 8, 1, 1)
+    assert not abr._fusable(a, s)
+    assert torch.equal(abr(a, s), torch.relu(a + abr.bias_a.view(1, -1, 1, 1) + s))
+
+
+@pytest.mark.gpu
+def test_gpu_fuse_guards_non_resnet_patterns():
+    """The rewritten aux-branch / broadcast-add network on the GPU: outputs and input gradients
+    equal the original module's (fp32; kernels and torch compute the same adds)."""
+    from wam_amd import model_fuse
+    torch.manual_seed(0)
+    net = _AuxBranchNet().eval().cuda()
+    gm = model_fuse.fuse_elementwise(torch.fx.symbolic_trace(net))[0]
+    x = torch.randn(3, 3, 16, 16, device="cuda")
+    outs = []
+    for m in (net, gm):
+        xx = x.clone().requires_grad_(True)
+        o = m(xx)
+        (g,) = torch.autograd.grad(o[:, 1].sum(), xx)
+        outs.append((o.detach(), g))
+    assert torch.allclose(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-6)
+    assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-6)
+
+
 def test_fuse_not_applied_on_cpu():
     gm = optimize_for_input_grad(testmodels.resnet18(seed=0))
     assert not any(type(m).__name__ == "ConvBiasReLU" for m in gm.modules())

@@ -37,13 +37,16 @@ def _is_int_label(y):
     return isinstance(y, (int, np.integer)) or (isinstance(y, torch.Tensor) and y.dim() == 0)
 
 
-def seed_gradient(out, y, groups, n):
-    """d loss / d out for `groups` stacked reference calls of n items each."""
+def seed_gradient(out, y, groups, n, unit=False):
+    """d loss / d out for `groups` stacked reference calls of n items each.
+    unit=True: the seed holds 1.0 where the loss gradient is non-zero and the loss scale (1/N^2,
+    1/N or 1/k) is returned beside it, so a low-precision model output (bf16) does not round the
+    scale -- the caller applies it to the fp32 input gradient. Returns (seed, scale or None)."""
     go = torch.zeros_like(out, dtype=torch.float32)
     rows = torch.arange(groups * n, device=out.device)
     if _is_int_label(y):
         val = torch.tensor(1.0, dtype=torch.float32) / (n * n)
-        go[rows, int(y)] = val.to(out.device)
+        rr, cc = rows, torch.full((groups * n,), int(y), dtype=torch.long, device=out.device)
     else:
         yy = torch.as_tensor(np.asarray([int(v) for v in (y.tolist() if isinstance(y, torch.Tensor) else y)]),
                              dtype=torch.long)
@@ -52,13 +55,16 @@ def seed_gradient(out, y, groups, n):
             k = min(n, yy.numel())
             val = torch.tensor(1.0, dtype=torch.float32) / k
             sel = torch.arange(k)
-            rr = (torch.arange(groups)[:, None] * n + sel[None, :]).reshape(-1)
-            cc = yy[:k].repeat(groups)
-            go[rr.to(out.device), cc.to(out.device)] = val.to(out.device)
-            return go.to(out.dtype)
-        val = torch.tensor(1.0, dtype=torch.float32) / n
-        go[rows, yy.repeat(groups).to(out.device)] = val.to(out.device)
-    return go.to(out.dtype)
+            rr = (torch.arange(groups)[:, None] * n + sel[None, :]).reshape(-1).to(out.device)
+            cc = yy[:k].repeat(groups).to(out.device)
+        else:
+            val = torch.tensor(1.0, dtype=torch.float32) / n
+            rr, cc = rows, yy.repeat(groups).to(out.device)
+    if unit:
+        go[rr, cc] = 1.0
+        return go.to(out.dtype), float(val)
+    go[rr, cc] = val.to(out.device)
+    return go.to(out.dtype), None
 
 
 def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=False, y_none_mean=False,
@@ -74,7 +80,10 @@ def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=
         loss = out.float().mean()
         (g,) = torch.autograd.grad(loss, img)
     else:
-        (g,) = torch.autograd.grad(out, img, grad_outputs=seed_gradient(out, y, groups, n))
+        seed, scale = seed_gradient(out, y, groups, n, unit=out.dtype != torch.float32)
+        (g,) = torch.autograd.grad(out, img, grad_outputs=seed)
+        if scale is not None:
+            g = g * scale
     return g.contiguous()
 
 

@@ -69,7 +69,8 @@ def smooth_frame(plan, n, frame, device):
             r = 2 * plan.band_shapes[-1][1]  # img_size = 2 * finest horizontal width (:217)
             src, band = _mosaic_2d(plan, (r, r), (224, 224))
             if (r, r) != (H, W):
-                _CACHE[key] = _bcast_error((n, H, W), (n, r, r))
+                # cache the geometry only: the message carries the batch size of each call
+                _CACHE[key] = lambda n_, r=r: _bcast_error((n_, H, W), (n_, r, r))
             else:
                 _CACHE[key] = (_to_dev(src, band, device), (r, r))
         elif frame == "native":
@@ -78,8 +79,8 @@ def smooth_frame(plan, n, frame, device):
         else:
             raise ValueError("frame must be 'legacy' or 'native'")
     v = _CACHE[key]
-    if isinstance(v, Exception):
-        raise ValueError(*v.args)
+    if callable(v):
+        raise v(n)
     return v
 
 
@@ -95,9 +96,9 @@ def ig_frames(plan, n, frame, device):
             gsrc, gband = gsrc[:224, :224], gband[:224, :224]
             bsrc, bband = _mosaic_2d(plan, (224, 224), (224, 224))
             if gsrc.shape != (H, W):
-                err = ValueError("could not broadcast input array from shape %s into shape %s" % (
-                    str((n,) + gsrc.shape).replace(" ", ""), str((n, H, W)).replace(" ", "")))
-                _CACHE[key] = err
+                _CACHE[key] = lambda n_, gs=gsrc.shape: ValueError(
+                    "could not broadcast input array from shape %s into shape %s" % (
+                        str((n_,) + gs).replace(" ", ""), str((n_, H, W)).replace(" ", "")))
             else:
                 _CACHE[key] = (_to_dev(bsrc, bband, device), _to_dev(gsrc, gband, device), (224, 224))
         elif frame == "native":
@@ -106,8 +107,8 @@ def ig_frames(plan, n, frame, device):
         else:
             raise ValueError("frame must be 'legacy' or 'native'")
     v = _CACHE[key]
-    if isinstance(v, Exception):
-        raise ValueError(*v.args)
+    if callable(v):
+        raise v(n)
     return v
 
 

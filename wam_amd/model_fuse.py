@@ -366,7 +366,25 @@ class AddBiasReLU(nn.Module):
         self.link_in = None   # _SkipLink: operand s comes from a linked producer (park its gradient)
         self.link_out = None  # _SkipLink: this output is a linked consumer's skip operand (take it)
 
+    def _fusable(self, a, s):
+        """The HIP kernel indexes s with a's flat index: same shape, dtype, layout and device only."""
+        if not (a.is_cuda and s.is_cuda and a.device == s.device and a.dtype == s.dtype and a.dtype in _DT
+                and a.shape == s.shape and a.dim() >= 2):
+            return False
+        for b in (self.bias_a, self.bias_s):
+            if b is not None and (b.dim() != 1 or b.numel() != a.shape[1]):
+                return False
+        return True
+
     def forward(self, a, s):
+        if not self._fusable(a, s):
+            # broadcast / mixed operands (e.g. relu(x + pos_embed)): plain torch, no skip hand-off
+            if self.link_out is not None:
+                self.link_out.cur = None
+            if self.link_in is not None:
+                self.link_in.cur = None
+            bias = (lambda t, b: t if b is None else t + b.to(t.dtype).view((1, -1) + (1,) * (t.dim() - 2)))
+            return torch.relu(bias(a, self.bias_a) + bias(s, self.bias_s))
         park = take = None
         if self.link_in is not None and self.link_in.cur is not None and torch.is_grad_enabled():
             park, self.link_in.cur = self.link_in.cur, None
@@ -537,6 +555,20 @@ def fuse_elementwise(gm):
     return gm, count
 
 
+def _reaches(src, dst):
+    """True when fx node dst is src or one of its (transitive) users."""
+    seen, stack = set(), [src]
+    while stack:
+        n = stack.pop()
+        if n is dst:
+            return True
+        if n in seen:
+            continue
+        seen.add(n)
+        stack.extend(n.users)
+    return False
+
+
 def _link_skip_gradients(gm, mods):
     """Link each identity residual block's AddBiasReLU with the AddBiasReLU that produced its skip
     operand, when that output has exactly two users: the block's conv1 and the add (_SkipGrad)."""
@@ -549,6 +581,12 @@ def _link_skip_gradients(gm, mods):
             continue
         add = [u for u in users if u.op == "call_module" and type(mods.get(u.target)) is AddBiasReLU]
         if len(add) != 1 or len(add[0].args) != 2 or add[0].args[1] is not node or add[0].args[0] is node:
+            continue
+        # the parked gradient is only complete if autograd runs the consumer before the producer:
+        # true when the producer's other user feeds the consumer's `a` operand (then the
+        # consumer's backward precedes every gradient that reaches the producer through it)
+        other = [u for u in users if u is not add[0]]
+        if len(other) != 1 or not _reaches(other[0], add[0].args[0]):
             continue
         link = _SkipLink()
         mods[node.target].link_out = link

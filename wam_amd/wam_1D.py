@@ -169,7 +169,10 @@ class WaveletAttribution1D(BaseWAM1D):
         if self.noise == "numpy":
             noise_it = legacy_noise([float(v) for v in sigma.cpu().numpy()], (w,), self.random_seed,
                                     list(range(s_lo, s_hi)))
-        mel_acc = None
+        # accumulators exist before the loop: a rank whose sample range is empty (n_samples <
+        # world size) still joins the all-reduce with zeros
+        self._mel_shape = (n, 1, plan.rec_shape[0] // (self.n_fft // 2) + 1, self.n_mels)
+        mel_acc = torch.zeros(int(np.prod(self._mel_shape)), dtype=torch.float32, device=dev)
         c_acc = torch.zeros(n * plan.coeff_numel, dtype=torch.float32, device=dev)
         for s0, cnt in chunks(s_lo, s_hi, group):
             host = None
@@ -178,9 +181,9 @@ class WaveletAttribution1D(BaseWAM1D):
             noisy = noise_add(x, sigma, cnt, n, w, w, seed=self.random_seed, sample_base=s0, host_noise=host)
             flat = plan.wavedec(noisy.view(cnt * n, w))
             g_mel, cg = self._grads(plan, flat, cnt * n, y, cnt, n)
-            if mel_acc is None:
-                mel_acc = torch.zeros(g_mel.numel() // cnt, dtype=torch.float32, device=dev)
-                self._mel_shape = (n,) + tuple(g_mel.shape[1:])
+            if g_mel.numel() != cnt * mel_acc.numel():
+                raise RuntimeError("melspec gradient shape %s does not match %s" % (tuple(g_mel.shape),
+                                                                                     self._mel_shape))
             accumulate_f32(g_mel, cnt, mel_acc)
             for b in range(plan.nbands):
                 nb = int(np.prod(plan.band_shapes[b]))
