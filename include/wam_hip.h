@@ -52,9 +52,12 @@ int wam_plan_create(wam_plan** plan, int ndim, const int64_t* shape, int levels,
                     const double* rec_lo, const double* rec_hi, int filt_len, int mode);
 /* flags: WAM_PLAN_GENERIC forces the per-axis kernels, WAM_PLAN_NO_ROWS skips the row-resident
  * and plane-resident 2D kernels, WAM_PLAN_NO_PLANE skips only the plane-resident (all levels in
- * one workgroup) kernels (all used by tests to cross-check the fused 2D kernels); 0 selects the
- * fastest path. wam_plan_create == wam_plan_create_ex(..., 0). */
-enum wam_plan_flags { WAM_PLAN_GENERIC = 1, WAM_PLAN_NO_ROWS = 2, WAM_PLAN_NO_PLANE = 4 };
+ * one workgroup) kernels; WAM_PLAN_NO_COOP / WAM_PLAN_FORCE_COOP pick the plane kernels' level-1
+ * form (wave chunks / cooperative row stream) instead of the size-based choice (all used by tests
+ * to cross-check the fused 2D kernels); 0 selects the fastest path.
+ * wam_plan_create == wam_plan_create_ex(..., 0). */
+enum wam_plan_flags { WAM_PLAN_GENERIC = 1, WAM_PLAN_NO_ROWS = 2, WAM_PLAN_NO_PLANE = 4, WAM_PLAN_NO_COOP = 8,
+                      WAM_PLAN_FORCE_COOP = 16 };
 int wam_plan_create_ex(wam_plan** plan, int ndim, const int64_t* shape, int levels,
                        const double* dec_lo, const double* dec_hi,
                        const double* rec_lo, const double* rec_hi, int filt_len, int mode, int flags);
@@ -204,6 +207,16 @@ int wam_trapz_f32(int64_t groups, int64_t k0, int64_t len, const float* src, con
  * upsampling to size x size; with approx, out[item, J] = upsampled approximation corner. */
 int wam_reproject_scales(int64_t items, int size, int levels, int approx, const double* avg,
                          double* out, void* stream);
+
+/* BaseWAM2D.scales (lib/wam_2D.py:133-198 disentangle_scales): maps = item-major |channel mean|
+ * coefficient-gradient maps of `items` images (wam_subband_maps / wam_waverec_adjoint_maps with one
+ * group), band_max = their per-band maxima over the batch. out[item, j] (j < levels, finest
+ * first) = (V + D) + H, each band / band_max upsampled to size x size (cv2 INTER_LINEAR on float32,
+ * half-pixel centres) in float32, stored as float64; with approx, out[items-1, levels] = the
+ * upsampled normalised approximation and out[i < items-1, levels] = 0 (the reference writes only
+ * its stale loop index, :194-197). out: [items, levels (+1), size, size] float64. */
+int wam_disentangle_scales(const wam_plan* plan, int64_t items, const float* maps, const float* band_max,
+                           int approx, int size, double* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Explained-model input-gradient pass (lib/wam_2D.py:114-116: model forward, diag-mean loss,

@@ -144,6 +144,31 @@ def ig_2d(model, x, y, wavelet="haar", J=3, mode="reflect", n_samples=25, normal
     return baseline * integral
 
 
+def disentangle_scales_2d(grads, J, approx_coeffs=False):
+    """BaseWAM2D.disentangle_scales (lib/wam_2D.py:133-198) on numpy coefficient gradients,
+    float32 maps as in the reference (mean over C, |.|, / batch max, cv2 resize, (V + D) + H);
+    the approximation row is written for the stale loop index only (:194-197)."""
+    n = grads[0].shape[0]
+    size = int(2 * grads[-1][0].shape[-1])
+    vis = np.zeros((n, J + 1 if approx_coeffs else J, size, size))
+    img_batch = None
+    for i, (h, v, d) in enumerate(grads[1:][::-1]):
+        h = np.abs(h.mean(axis=1))
+        h /= h.max()
+        d = np.abs(d.mean(axis=1))
+        d /= d.max()
+        v = np.abs(v.mean(axis=1))
+        v /= v.max()
+        for img_batch in range(n):
+            vis[img_batch, i] = bilinear_resize(v[img_batch], (size, size)) + \
+                bilinear_resize(d[img_batch], (size, size)) + bilinear_resize(h[img_batch], (size, size))
+    if approx_coeffs:
+        a = np.abs(grads[0].mean(axis=1))
+        a /= a.max()
+        vis[img_batch, J] = bilinear_resize(a[img_batch], (size, size))
+    return vis
+
+
 def bilinear_resize(a, out_hw):
     """cv2.resize(a, (w, h), INTER_LINEAR) for upsampling (half-pixel centres, edge clamp)."""
     t = torch.as_tensor(np.ascontiguousarray(a))[None, None]

@@ -56,3 +56,14 @@ def make_model(case):
     if case["model"] == "tinyvoxel":
         return testmodels.TinyVoxel()
     raise KeyError(case["model"])
+
+
+# BaseWAM2D single passes with their .scales (disentangle_scales) -- make_base_goldens.py
+BASE_CASES = {
+    # approx row written for the last image only (stale img_batch); list y
+    "b2_haar_approx": dict(dim=2, shape=(3, 3, 224, 224), seed=201, y=[1, 4, 2], model="tiny2d",
+                           kw=dict(wavelet="haar", J=3, mode="reflect", approx_coeffs=True)),
+    # db4 at 224: .scales canvas 230 (2 * finest width), int y, symmetric mode
+    "b2_db4_int": dict(dim=2, shape=(2, 3, 224, 224), seed=202, y=6, model="tiny2d",
+                       kw=dict(wavelet="db4", J=2, mode="symmetric", approx_coeffs=False)),
+}

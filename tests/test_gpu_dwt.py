@@ -344,20 +344,21 @@ def test_haar3_blocks_equal_per_axis(wam, shape, J, mode):
                                               ("db2", (64, 96), 4, "symmetric"), ("db3", (100, 84), 2, "zero"),
                                               ("db4", (37, 52), 2, "reflect"), ("sym4", (36, 200), 3, "constant"),
                                               ("db4", (224, 224), 1, "periodic"), ("db4", (17, 16), 3, "reflect")])
-def test_plane_coop_equals_wave_chunks(wam, wav, shape, J, mode, monkeypatch):
-    """Cooperative level-1 row stream (WAM_PLANE_COOP=1) vs the wave-chunk form (=0): the same
-    taps in the same fma order, so wavedec, noisy wavedec and the maps epilogue are bit-identical."""
-    p = wam.get_plan(2, shape, J, wav, mode, "cuda")
-    if not p.caps & wam.CAP_NOISY_WAVEDEC:
+def test_plane_coop_equals_wave_chunks(wam, wav, shape, J, mode):
+    """Cooperative level-1 row stream (plan flag WAM_PLAN_FORCE_COOP) vs the wave-chunk form
+    (WAM_PLAN_NO_COOP): the same taps in the same fma order, so wavedec, noisy wavedec and the
+    maps epilogue are bit-identical."""
+    plans = {"0": wam.get_plan(2, shape, J, wav, mode, "cuda", flags=wam.PLAN_NO_COOP),
+             "1": wam.get_plan(2, shape, J, wav, mode, "cuda", flags=wam.PLAN_FORCE_COOP)}
+    if not all(p.caps & wam.CAP_NOISY_WAVEDEC for p in plans.values()):
         pytest.skip("plane kernels do not cover this geometry")
     torch.manual_seed(11)
     N, C, S = 3, 3, 4
     x = torch.randn((N, C) + shape, device="cuda")
     sigma = wam.item_sigma(x, C * shape[0] * shape[1], C * shape[0] * shape[1], 0.25)
-    g = torch.randn((S * N * C,) + p.rec_shape, device="cuda")
+    g = torch.randn((S * N * C,) + plans["0"].rec_shape, device="cuda")
     out = {}
-    for flag in ("0", "1"):
-        monkeypatch.setenv("WAM_PLANE_COOP", flag)
+    for flag, p in plans.items():
         out[flag] = (p.wavedec(x.view(N * C, *shape)),
                      p.wavedec_noisy(x, sigma, S, N, C, seed=5, sample_base=2),
                      p.adjoint(g),

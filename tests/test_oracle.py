@@ -12,7 +12,7 @@ import pytest
 import torch
 
 from oracle import dwt, ptwt_torch, wam_ref
-from tests.golden.glue_cases import CASES, make_inputs, make_model
+from tests.golden.glue_cases import BASE_CASES, CASES, make_inputs, make_model
 from tests.helpers import flat_bands, max_rel, npz, pywt_cases, pywt_coeffs
 
 
@@ -91,6 +91,25 @@ def test_glue_oracle_vs_reference_goldens(name):
     else:
         r = (wam_ref.smooth_3d if method == "smooth" else wam_ref.ig_3d)(m, x, y, **kw)
         assert max_rel(r, g[name]) < 1e-6
+
+
+@pytest.mark.parametrize("name", list(BASE_CASES))
+def test_disentangle_scales_oracle_vs_reference_goldens(name):
+    """Row a8: the BaseWAM2D single pass and its .scales (disentangle_scales, incl. the stale
+    approximation index) restated in oracle/wam_ref.py vs the reference's own outputs."""
+    case = BASE_CASES[name]
+    g = npz("base_goldens.npz")
+    x, y = make_inputs(case)
+    kw = case["kw"]
+    _, grads = wam_ref.single_pass_2d(make_model(case), x, y, kw["wavelet"], kw["J"], kw["mode"])
+    size = 2 * grads[-1][0].shape[-1]
+    canvas = wam_ref.mosaic_2d(grads, True, (size, size), (224, 224))
+    assert np.abs(canvas - g[name]).max() < 1e-9
+    sc = wam_ref.disentangle_scales_2d(grads, kw["J"], kw["approx_coeffs"])
+    assert sc.shape == g[name + "_scales"].shape
+    assert np.abs(sc - g[name + "_scales"]).max() < 1e-9
+    if kw["approx_coeffs"]:
+        assert not sc[:-1, kw["J"]].any() and sc[-1, kw["J"]].any()
 
 
 def test_level_sizes_match_survey():

@@ -53,6 +53,7 @@ _SIGS = {
     "wam_accumulate_f32": (c_int, [c_i64, c_i64, c_vp, c_f32, c_vp, c_vp]),
     "wam_trapz_f32": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "wam_reproject_scales": (c_int, [c_i64, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
+    "wam_disentangle_scales": (c_int, [c_vp, c_i64, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
     "wam_plan_caps": (c_int, [c_vp]),
     "wam_wavedec_noisy": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, ctypes.c_uint64, c_i64, c_vp, c_vp, c_vp]),
     "wam_waverec_adjoint_maps": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -23,8 +23,6 @@
 // Workgroup order: an XCD-aware bijective swizzle makes consecutive logical workgroups share an
 // XCD (L2); for noisy analysis the logical order is sample-fastest, so the S noise samples of one
 // clean plane run back to back on one XCD and its rows are read from HBM about once.
-#include <stdlib.h>
-
 #include <atomic>
 
 #include "rowtools.hpp"
@@ -769,11 +767,10 @@ int coop_lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap) {
 }
 
 bool coop_ok(const wam_plan* p, int nw0) {
-  const char* e = getenv("WAM_PLANE_COOP");
-  if (e && e[0] == '0') return false;
+  if (p->flags & WAM_PLAN_NO_COOP) return false;
   if (p->lout[0][1] > 128 || p->pad > kCoopPadL) return false;
   int rowlds, llcap;
-  return (int64_t)coop_lds_floats(p, nw0, rowlds, llcap) * 4 <= kTwoWgLds || (e && e[0] == '1');
+  return (int64_t)coop_lds_floats(p, nw0, rowlds, llcap) * 4 <= kTwoWgLds || (p->flags & WAM_PLAN_FORCE_COOP);
 }
 
 int lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap) {
@@ -822,8 +819,7 @@ PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items
   g.maps_item = p->band_off[p->nbands];
   lds_floats(p, nw0, g.rowlds, g.llcap);
   g.coop = coop_ok(p, nw0);
-  const char* o = getenv("WAM_NOISE_ORDER");
-  g.sample_fast = !(o && o[0] == 'p');
+  g.sample_fast = 1;
   return g;
 }
 

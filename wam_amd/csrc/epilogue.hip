@@ -377,6 +377,66 @@ __global__ void __launch_bounds__(256) k_reproject(int64_t items, int size, int 
   }
 }
 
+
+// BaseWAM2D.disentangle_scales (lib/wam_2D.py:133-198): per image and level (finest first) the
+// sum (V + D) + H of the batch-max-normalised |channel mean| maps, each upsampled to size x size
+// by cv2 INTER_LINEAR on float32 data (half-pixel centres, edge clamp; torch's bilinear on the
+// reference's float32 arrays), stored as float64; with approx the normalised approximation of the
+// LAST image only (the reference's stale loop variable, :194-197).
+struct ScalesGeom {
+  int J;
+  int nbands;
+  int64_t item;                        // floats per item of the packed maps
+  int64_t off[WAM_MAX_LEVELS][3];      // H, V, D offsets of level l (0 = finest)
+  int band[WAM_MAX_LEVELS][3];
+  int mh[WAM_MAX_LEVELS], mw[WAM_MAX_LEVELS];
+  int64_t off_a;
+};
+
+__device__ __forceinline__ float bilinear_f32(const float* __restrict__ m, float band_mx, int ih, int iw, int oy,
+                                              int ox, int out) {
+  float sy = ((float)ih / (float)out) * ((float)oy + 0.5f) - 0.5f;
+  float sx = ((float)iw / (float)out) * ((float)ox + 0.5f) - 0.5f;
+  sy = sy < 0.f ? 0.f : sy;
+  sx = sx < 0.f ? 0.f : sx;
+  const int y0 = (int)sy, x0 = (int)sx;
+  const float ly1 = fminf(sy - (float)y0, 1.f), lx1 = fminf(sx - (float)x0, 1.f);
+  const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+  const int y1 = y0 + (y0 < ih - 1 ? 1 : 0), x1 = x0 + (x0 < iw - 1 ? 1 : 0);
+  // the normalised map value first (numpy's a /= a.max()), then the interpolation
+  const float v00 = m[(int64_t)y0 * iw + x0] / band_mx, v01 = m[(int64_t)y0 * iw + x1] / band_mx;
+  const float v10 = m[(int64_t)y1 * iw + x0] / band_mx, v11 = m[(int64_t)y1 * iw + x1] / band_mx;
+  return (v00 * lx0 + v01 * lx1) * ly0 + (v10 * lx0 + v11 * lx1) * ly1;
+}
+
+__global__ void __launch_bounds__(256) k_disentangle(int64_t items, int size, int approx, ScalesGeom g,
+                                                     const float* __restrict__ maps, const float* __restrict__ bmax,
+                                                     double* __restrict__ out) {
+  const int nl = g.J + (approx ? 1 : 0);
+  const int64_t plane = (int64_t)size * size;
+  const int64_t total = items * nl * plane;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pix = t % plane;
+    const int64_t q = t / plane;
+    const int j = (int)(q % nl);
+    const int64_t it = q / nl;
+    const int oy = (int)(pix / size), ox = (int)(pix % size);
+    const float* m = maps + it * g.item;
+    double v;
+    if (j < g.J) {
+      const int ih = g.mh[j], iw = g.mw[j];
+      const float h = bilinear_f32(m + g.off[j][0], bmax[g.band[j][0]], ih, iw, oy, ox, size);
+      const float vv = bilinear_f32(m + g.off[j][1], bmax[g.band[j][1]], ih, iw, oy, ox, size);
+      const float d = bilinear_f32(m + g.off[j][2], bmax[g.band[j][2]], ih, iw, oy, ox, size);
+      v = (double)((vv + d) + h);
+    } else {
+      v = it == items - 1 ? (double)bilinear_f32(m + g.off_a, bmax[0], g.mh[g.J - 1], g.mw[g.J - 1], oy, ox, size)
+                          : 0.0;
+    }
+    out[t] = v;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -516,6 +576,31 @@ int wam_reproject_scales(int64_t items, int size, int levels, int approx, const 
   if (work == 0) return WAM_OK;
   hipLaunchKernelGGL(k_reproject, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, items, size, levels,
                      approx, avg, out);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int wam_disentangle_scales(const wam_plan* plan, int64_t items, const float* maps, const float* band_max, int approx,
+                           int size, double* out, void* stream) {
+  if (!plan || plan->ndim != 2 || items < 0 || size < 1 || !maps || !band_max || !out) return WAM_ERR_INVALID_ARG;
+  ScalesGeom g{};
+  g.J = plan->levels;
+  g.nbands = plan->nbands;
+  g.item = plan->band_off[plan->nbands];
+  for (int l = 0; l < plan->levels; ++l) {
+    g.mh[l] = (int)plan->lout[l][0];
+    g.mw[l] = (int)plan->lout[l][1];
+    for (int k = 0; k < 3; ++k) {
+      g.band[l][k] = wam_band_of(plan, l, k);
+      g.off[l][k] = plan->band_off[g.band[l][k]];
+    }
+  }
+  g.off_a = plan->band_off[0];
+  const int64_t work = items * (plan->levels + (approx ? 1 : 0)) * (int64_t)size * size;
+  if (work == 0) return WAM_OK;
+  WamTimer tm((hipStream_t)stream, "k_disentangle", 4.0 * items * g.item + 8.0 * work);
+  hipLaunchKernelGGL(k_disentangle, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, items, size, approx,
+                     g, maps, band_max, out);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }

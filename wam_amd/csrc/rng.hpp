@@ -44,16 +44,8 @@ __device__ __forceinline__ void wam_box_muller(uint32_t a, uint32_t b, float& z0
 // four N(0,1) values for element group g of `item` in `sample`
 __device__ __forceinline__ void wam_normal4(int64_t g, int64_t item, int64_t sample, uint32_t k0, uint32_t k1,
                                             float z[4]) {
-#if defined(WAM_NOISE_EXPERIMENT) && WAM_NOISE_EXPERIMENT == 1
-  z[0] = z[1] = z[2] = z[3] = 0.5f + 1e-9f * (float)g;
-  return;
-#endif
   wam_u4 c = {(uint32_t)g, (uint32_t)(g >> 32) ^ ((uint32_t)item << 8), (uint32_t)sample, (uint32_t)item};
   wam_u4 r = wam_philox4x32_10(c, k0, k1);
-#if defined(WAM_NOISE_EXPERIMENT) && WAM_NOISE_EXPERIMENT == 2
-  z[0] = (float)r.x; z[1] = (float)r.y; z[2] = (float)r.z; z[3] = (float)r.w;
-  return;
-#endif
   wam_box_muller(r.x, r.y, z[0], z[1]);
   wam_box_muller(r.z, r.w, z[2], z[3]);
 }

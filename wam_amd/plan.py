@@ -170,6 +170,8 @@ def get_plan(ndim, shape, levels, wavelet, mode, device, generic=False, flags=No
 
 PLAN_NO_ROWS = 2
 PLAN_NO_PLANE = 4
+PLAN_NO_COOP = 8
+PLAN_FORCE_COOP = 16
 CAP_NOISY_WAVEDEC = 1
 CAP_ADJOINT_MAPS = 2
 
@@ -264,4 +266,13 @@ def reproject_scales(avg, levels, approx):
     out = torch.empty((items, levels + (1 if approx else 0), size, size), dtype=torch.float64, device=avg.device)
     check(lib.wam_reproject_scales(items, size, levels, int(bool(approx)), ptr(avg.contiguous()), ptr(out),
                                    stream_of(avg.device)))
+    return out
+
+
+def disentangle_scales(plan, maps, band_max, items, approx, size):
+    """BaseWAM2D.disentangle_scales on device maps -> [items, J(+1), size, size] float64."""
+    out = torch.empty((items, plan.levels + (1 if approx else 0), size, size), dtype=torch.float64,
+                      device=maps.device)
+    check(lib.wam_disentangle_scales(plan.handle, items, ptr(maps), ptr(band_max), int(bool(approx)), int(size),
+                                     ptr(out), stream_of(maps.device)))
     return out

@@ -29,8 +29,8 @@ from . import frames
 from .constants import WaveletDetailTuple2d
 from .engine import (GradModel, Shard, auto_group, chunks, ig_weights, legacy_noise, model_device,
                      require_gpu_device, wam_group)
-from .plan import (CAP_ADJOINT_MAPS, CAP_NOISY_WAVEDEC, frame_accumulate, frame_trapz, get_plan, item_sigma,
-                   noise_add, reproject_scales, subband_maps)
+from .plan import (CAP_ADJOINT_MAPS, CAP_NOISY_WAVEDEC, disentangle_scales, frame_accumulate, frame_trapz,
+                   get_plan, item_sigma, noise_add, reproject_scales, subband_maps)
 
 
 def _to_numpy_2d(plan, flat, batch_items, n, c, first_item=0):
@@ -163,8 +163,20 @@ class BaseWAM2D:
     @property
     def scales(self):
         if self._scales is None and self._pass is not None:
-            self._scales = self.disentangle_scales(self.gradient_coeffs, approx_coeffs=self.approx_coeffs)
+            self._scales = self._scales_dev()
         return self._scales
+
+    def _scales_dev(self):
+        """disentangle_scales of the recorded pass on the GPU: coefficient gradients -> |channel
+        mean| maps + batch maxima (wam_subband_maps) -> bilinear reprojection (k_disentangle)."""
+        plan, _, (gf, b, f), n, c, gimg = self._pass
+        if gimg is not None:
+            gf, b, f = plan.adjoint(gimg), n * c, 0
+        views = plan.split(gf, b)
+        cg = torch.cat([v[f * c:(f + n) * c].reshape(-1) for v in views])  # this pass's n*c items
+        maps, bmax = subband_maps(plan, cg, 1, n, c)
+        size = int(2 * plan.band_shapes[-1][1])
+        return disentangle_scales(plan, maps, bmax, n, self.approx_coeffs, size).cpu().numpy()
 
     @scales.setter
     def scales(self, v):
