@@ -111,6 +111,12 @@ int wam_plan_caps(const wam_plan* plan);
 int wam_wavedec_noisy(const wam_plan* plan, int64_t n_samples, int64_t images, int channels,
                       const float* x, const float* sigma, uint64_t seed, int64_t sample_base,
                       float* coeffs, void* workspace, void* stream);
+/* the same with the Philox image counter offset by image_base: x holds images [image_base,
+ * image_base + images) of a batch sharded over ranks, so every image keeps the noise it gets
+ * unsharded (wam_wavedec_noisy == image_base 0) */
+int wam_wavedec_noisy_ex(const wam_plan* plan, int64_t n_samples, int64_t images, int channels,
+                         const float* x, const float* sigma, uint64_t seed, int64_t sample_base,
+                         int64_t image_base, float* coeffs, void* workspace, void* stream);
 
 /* Backward pass of waverec fused with the WAM epilogue (lib/wam_2D.py:116 loss.backward() through
  * ptwt.waverec2, then :227-256 channel mean, |.|, batch-global max): for every image
@@ -145,6 +151,10 @@ int wam_item_sigma(int64_t items, int64_t item_stride, int64_t len, const float*
 int wam_noise_add(int64_t n_samples, int64_t items, int64_t item_stride, int64_t noised_len,
                   const float* x, const float* sigma, const float* host_noise, uint64_t seed,
                   int64_t sample_base, float* out, void* stream);
+/* the same with the Philox item counter offset by item_base (items of a batch-sharded rank) */
+int wam_noise_add_ex(int64_t n_samples, int64_t items, int64_t item_stride, int64_t noised_len,
+                     const float* x, const float* sigma, const float* host_noise, uint64_t seed,
+                     int64_t sample_base, int64_t item_base, float* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Per-subband reduction and accumulation (lib/wam_2D.py:200-264 visualize_grad_wam,

@@ -1,0 +1,86 @@
+"""World-2 run of the WAM classes with dist=... (one process per rank, both on cuda:0, gloo).
+
+Launched by tests/conftest.py BEFORE the pytest process touches the GPU (a process that has
+initialised the GPU must not start programs itself):
+
+    python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port P tests/dist_worker.py OUT.json
+
+Every rank computes each case twice -- unsharded (dist=None) and sharded (dist=True, the given
+dist_axis) -- and rank 0 writes {case: max |sharded - unsharded| / max(1, max |unsharded|)} plus
+any exception text to OUT.json. Cases cover SURVEY 8(e): ragged sample / step splits, batch
+(image) sharding with the all-reduce MAX of the batch-global maxima, int-y loss scaling with
+unnormalised maps, 1D with fewer samples than ranks (an empty range), 3D legacy weights, IG.
+"""
+import json
+import os
+import sys
+import traceback
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def cases():
+    import testmodels
+    rs = np.random.RandomState(31)
+    x2 = torch.tensor(rs.standard_normal((3, 3, 224, 224)).astype(np.float32))
+    x96 = torch.tensor(rs.standard_normal((3, 3, 96, 96)).astype(np.float32))
+    x1 = torch.tensor(rs.standard_normal((3, 4000)).astype(np.float32))
+    x3 = torch.tensor((rs.standard_normal((2, 1, 16, 16, 16)) > 0).astype(np.float32))
+    m2, m1, m3 = testmodels.TinySmooth2D, testmodels.TinyAudio, testmodels.TinyVoxel
+    yield ("2d_smooth_numpy_samples", "2D", m2, x2, [1, 4, 2],
+           dict(wavelet="haar", J=3, n_samples=5, dist_axis="samples"))
+    yield ("2d_smooth_philox_images", "2D", m2, x2, [1, 4, 2],
+           dict(wavelet="db4", J=3, n_samples=4, noise="philox", frame="native", dist_axis="images"))
+    yield ("2d_smooth_numpy_images_int_y_unnormalised", "2D", m2, x2, 5,
+           dict(wavelet="haar", J=2, n_samples=3, normalize_coeffs=False, dist_axis="images"))
+    yield ("2d_ig_samples", "2D", m2, x96, [0, 1, 2],
+           dict(wavelet="db4", J=2, method="integratedgrad", n_samples=5, frame="native", dist_axis="samples"))
+    yield ("2d_ig_images", "2D", m2, x96, [0, 1, 2],
+           dict(wavelet="sym4", J=2, method="integratedgrad", n_samples=4, frame="native", dist_axis="images"))
+    yield ("1d_smooth_one_sample", "1D", m1, x1, [1, 2, 3],
+           dict(wavelet="db6", J=3, n_samples=1, sample_rate=16000))
+    yield ("1d_smooth", "1D", m1, x1, [1, 2, 3], dict(wavelet="db6", J=3, n_samples=3, sample_rate=16000))
+    yield ("1d_ig", "1D", m1, x1, 4, dict(wavelet="haar", J=3, method="integratedgrad", n_samples=3,
+                                          sample_rate=16000))
+    yield ("3d_smooth_legacy_weights", "3D", m3, x3, [1, 2], dict(wavelet="haar", J=2, n_samples=3,
+                                                                  stdev_spread=0.05))
+    yield ("3d_ig", "3D", m3, x3, [1, 2], dict(wavelet="haar", J=2, method="integratedgrad", n_samples=3))
+
+
+def flat(r):
+    if isinstance(r, tuple):  # 1D: (melspec grads, [coefficient grads])
+        return np.concatenate([np.asarray(r[0]).ravel()] + [np.asarray(c).ravel() for c in r[1]])
+    return np.asarray(r).ravel()
+
+
+def main():
+    out_path = sys.argv[1]
+    dist.init_process_group("gloo")
+    rank = dist.get_rank()
+    torch.cuda.set_device(0)
+    import wam_amd
+    res = {}
+    for name, dim, model, x, y, kw in cases():
+        try:
+            cls = getattr(wam_amd, "WaveletAttribution" + dim)
+            ref = flat(cls(model().cuda(), **kw)(x, y))
+            got = flat(cls(model().cuda(), dist=True, **kw)(x, y))
+            err = float(np.abs(got - ref).max() / max(1.0, np.abs(ref).max())) if got.shape == ref.shape else 1e9
+            res[name] = {"err": err, "shape_ok": got.shape == ref.shape}
+        except Exception:
+            res[name] = {"error": traceback.format_exc()}
+        dist.barrier()
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump(res, f, indent=1)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -25,7 +25,7 @@ def test_header_symbols_exported_and_bound():
 
 def test_host_only_entry_points():
     from wam_amd import _lib
-    assert _lib.lib.wam_version() == 1
+    assert _lib.lib.wam_version() == 2
     assert b"shape" in _lib.lib.wam_strerror(2)
     assert _lib.lib.wam_strerror(0) == b"success"
     # NULL plan arguments are rejected without touching the device

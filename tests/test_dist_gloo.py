@@ -63,6 +63,27 @@ def _worker(rank, world, port, q):
         part3 = (w3[:, None] * C[s0:s1]).sum(0)
         shard.all_reduce_sum(part3)
         res["cube"] = part3.numpy()
+        # --- 2D SmoothGrad, batch (image) axis: ragged image ranges, each rank's per-sample band
+        # maxima combined by an all-reduce MAX before normalising, rows gathered at the end (the
+        # classes' dist_axis='images'; the loss seed of a rank's rows: engine.seed_gradient batch=)
+        x3 = torch.tensor(np.random.RandomState(4).standard_normal((3, 3, 64, 64)).astype(np.float32))
+        i0, i1 = shard.range(3)
+        sig3 = [float(np.float32(0.25) * (x3[i].max() - x3[i].min())) for i in range(3)]
+        acc3 = torch.zeros(i1 - i0, 64, 64, dtype=torch.float64)
+        for s, noise in engine.legacy_noise(sig3, (3, 64, 64), 42, list(range(3))):
+            noisy = (x3 + torch.tensor(noise))[i0:i1]
+            _, g = wam_ref.single_pass_2d(model, noisy, [1, 2, 0][i0:i1], "db2", 2, "reflect")
+            bands = [np.abs(g[0].mean(axis=1))] + [np.abs(t.mean(axis=1)) for lv in g[1:] for t in lv]
+            # the oracle's loss is the mean over this rank's rows (1/n_local per item); the whole
+            # batch's loss scales every item by 1/N (what seed_gradient(batch=) seeds)
+            bands = [b * np.float32((i1 - i0) / 3.0) for b in bands]
+            mx = torch.tensor([float(b.max()) for b in bands], dtype=torch.float32)
+            shard.all_reduce_max(mx)
+            normed = [b / np.float32(m) for b, m in zip(bands, mx.numpy())]
+            gn = [normed[0][:, None]] + [tuple(normed[1 + 3 * k + j][:, None] for j in range(3))
+                                         for k in range(len(g) - 1)]
+            acc3 += torch.tensor(wam_ref.mosaic_2d(gn, False, (64, 64), (64, 64)))
+        res["smooth_images"] = (shard.all_gather_rows(acc3, 3) / 3).numpy()
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -94,3 +115,7 @@ def test_two_rank_sharding_matches_single_process():
         assert np.allclose(out[r]["ig"], np.trapz(G, axis=0), rtol=1e-5, atol=1e-6)
         assert np.allclose(out[r]["cube"], avg, rtol=1e-5, atol=1e-30)
         assert np.array_equal(out[0]["smooth"], out[r]["smooth"])
+        ref3 = wam_ref.smooth_2d(testmodels.TinySmooth2D(), torch.tensor(np.random.RandomState(4).standard_normal(
+            (3, 3, 64, 64)).astype(np.float32)), [1, 2, 0], wavelet="db2", J=2, n_samples=3, frame="native")
+        assert out[r]["smooth_images"].shape == ref3.shape
+        assert np.abs(out[r]["smooth_images"] - ref3).max() < 1e-6

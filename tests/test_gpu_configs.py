@@ -55,8 +55,7 @@ def test_alpha_fused_waverec_sym8_512_j5():
     """The per-level sym8 synthesis with the IG alpha fused on the coefficient load equals the
     synthesis of the pre-scaled coefficients fp32(alpha) * c, bit for bit (c4 geometry)."""
     from wam_amd import plan as P
-    p = P.get_plan(2, (512, 512), 5, "sym8", "reflect", "cuda")
-    assert not p.caps & P.CAP_NOISY_WAVEDEC  # sym8 runs the per-level kernels, not the plane ones
+    p = P.get_plan(2, (512, 512), 5, "sym8", "reflect", "cuda")  # 16 taps: per-level kernels
     torch.manual_seed(12)
     B = 6
     c = torch.randn(B * p.coeff_numel, device="cuda")

@@ -99,6 +99,19 @@ def test_seed_gradient_matches_autograd_of_reference_loss(y, n):
     assert torch.equal(gu * scale, g_ref)
 
 
+@pytest.mark.parametrize("y,n", [(3, 5), ([1, 5, 2, 2, 0], 5), ([4, 5], 5), (list(range(7)), 5)])
+def test_seed_gradient_batch_slices(y, n):
+    """A batch-sharded rank seeds exactly its rows of the whole batch's loss gradient."""
+    groups = 2
+    out = torch.randn(groups * n, 10)
+    full, _ = engine.seed_gradient(out, y, groups, n)
+    full = full.view(groups, n, 10)
+    for lo, hi in [(0, 2), (2, 4), (4, 5), (1, 5)]:
+        part, _ = engine.seed_gradient(out.view(groups, n, 10)[:, lo:hi].reshape(-1, 10), y, groups, hi - lo,
+                                       batch=(lo, n))
+        assert torch.equal(part.view(groups, hi - lo, 10), full[:, lo:hi])
+
+
 def test_input_gradient_bf16_scale_not_rounded():
     """The 1/N^2 loss scale is applied in fp32 after a bf16 backward (1/9 is not a bf16 value)."""
     torch.manual_seed(0)

@@ -44,6 +44,8 @@ _SIGS = {
     "wam_waverec_adjoint": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "wam_item_sigma": (c_int, [c_i64, c_i64, c_i64, c_vp, c_f32, c_vp, c_vp]),
     "wam_noise_add": (c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, ctypes.c_uint64, c_i64, c_vp, c_vp]),
+    "wam_noise_add_ex": (c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, ctypes.c_uint64, c_i64, c_i64, c_vp,
+                                 c_vp]),
     "wam_subband_maps": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
     "wam_frame_accumulate": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_vp, c_vp]),
     "wam_frame_trapz": (c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_vp, c_vp,
@@ -56,6 +58,8 @@ _SIGS = {
     "wam_disentangle_scales": (c_int, [c_vp, c_i64, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
     "wam_plan_caps": (c_int, [c_vp]),
     "wam_wavedec_noisy": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, ctypes.c_uint64, c_i64, c_vp, c_vp, c_vp]),
+    "wam_wavedec_noisy_ex": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, ctypes.c_uint64, c_i64, c_i64, c_vp, c_vp,
+                                     c_vp]),
     "wam_waverec_adjoint_maps": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "wam_timing_enable": (c_int, [c_int]),
     "wam_ew_bias_act": (c_int, [c_int, c_i64, c_i64, c_i64, c_vp, c_vp, c_int, c_vp]),

@@ -178,8 +178,8 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     auto hrow = [&](RowRegs<4, 1> (&fr)[NCH], int sr, int e) {
       float nzr[4];
       if constexpr (NOISE)
-        make_noise<1>(nzr, nw, lane, (ch * nh + (sr >= 0 ? sr : 0)) * (int64_t)nw, sg, img, smp, nz.k0, nz.k1,
-                      sr >= 0);
+        make_noise<1>(nzr, nw, lane, (ch * nh + (sr >= 0 ? sr : 0)) * (int64_t)nw, sg, img + nz.image_base, smp,
+                      nz.k0, nz.k1, sr >= 0);
       float4 o = fr[0].ok[0] ? make_float4(fr[0].v[0], fr[0].v[1], fr[0].v[2], fr[0].v[3])
                              : make_float4(0.f, 0.f, 0.f, 0.f);
       if constexpr (NCH > 1) {
@@ -354,8 +354,8 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
       // Philox work overlaps the row's load latency instead of following its vmcnt wait
       float nzr[4];
       if constexpr (NOISE)
-        make_noise<1>(nzr, nw, lane, (ch * nh + (sr >= 0 ? sr : 0)) * (int64_t)nw, sg, img, smp, nz.k0, nz.k1,
-                      sr >= 0);
+        make_noise<1>(nzr, nw, lane, (ch * nh + (sr >= 0 ? sr : 0)) * (int64_t)nw, sg, img + nz.image_base, smp,
+                      nz.k0, nz.k1, sr >= 0);
       RowRegs<4, 1> m = fr[0];
       if constexpr (NCH > 1) {
 #pragma unroll
@@ -890,7 +890,7 @@ int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in
     return dispatch_plane<true, 0, false>(p, g, lds_bytes, items, in, coeffs, nullptr, filt, *nz, n_samples, 1,
                                           "k_plane_ana<noise>", bytes, st);
   }
-  const WamNoise none{nullptr, 1, 1, 0, 0, 0};
+  const WamNoise none{nullptr, 1, 1, 0, 0, 0, 0};
   return dispatch_plane<false, 0, false>(p, g, lds_bytes, items, in, coeffs, nullptr, filt, none, 1, 1,
                                          "k_plane_ana", bytes, st);
 }
@@ -904,7 +904,7 @@ int launch_dwt2_plane_maps(const wam_plan* p, int64_t images, int channels, int6
   PlaneGeom g = make_geom(p, nh0, nw0, WAM_MODE_ZERO, images);
   int rowlds, llcap;
   const int lds_bytes = lds_floats(p, nw0, rowlds, llcap) * 4;
-  const WamNoise none{nullptr, 1, 1, 0, 0, 0};
+  const WamNoise none{nullptr, 1, 1, 0, 0, 0, 0};
   const double bytes = 4.0 * (double)images * ((double)channels * nh0 * nw0 + (double)p->band_off[p->nbands]);
   if (channels == 3)
     return dispatch_plane<false, 3, true>(p, g, lds_bytes, images, grad, maps, band_max, filt, none, 1, group_items,

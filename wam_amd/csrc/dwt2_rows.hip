@@ -83,7 +83,8 @@ __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, 
     const bool valid = sr >= 0;
     const int rr = valid ? sr : 0;
     r.fetch(src + (int64_t)rr * nw, nw, lane, valid);
-    if constexpr (NOISE) make_noise<MAXV>(nzr, nw, lane, (ch * nh + rr) * (int64_t)nw, sg, img, smp, nz.k0, nz.k1, valid);
+    if constexpr (NOISE) make_noise<MAXV>(nzr, nw, lane, (ch * nh + rr) * (int64_t)nw, sg, img + nz.image_base, smp, nz.k0, nz.k1,
+                                             valid);
   };
   auto process = [&](const RowRegs<VEC, MAXV>& r, const float (&nzr)[NZ], float (&lo)[CPL], float (&hi)[CPL]) {
     r.commit(lds, lane, NOISE ? nzr : nullptr, sg);
@@ -341,7 +342,7 @@ int launch_ana_rows_t(int64_t batch, const float* in, int nh, int nw, int mh, in
   int nchunks, R;
   pick_chunks(batch * nstrips, mh, nchunks, R);
   const int64_t waves = batch * nstrips * nchunks;
-  WamNoise z = nz ? *nz : WamNoise{nullptr, 1, 1, 0, 0, 0};
+  WamNoise z = nz ? *nz : WamNoise{nullptr, 1, 1, 0, 0, 0, 0};
   double bytes = 4.0 * ((double)batch * 4.0 * mh * mw + (nz ? (double)z.images * z.channels : (double)batch) * nh * nw);
   WamTimer tm(st, NOISE ? "k_ana_rows<noise>" : "k_ana_rows", bytes);
   hipLaunchKernelGGL((k_ana_rows<L, CPL, VEC, MAXV, NOISE>), dim3((unsigned)((waves + kWaves - 1) / kWaves)),

@@ -80,7 +80,8 @@ __global__ void __launch_bounds__(256) k_noise_add(int64_t n_samples, int64_t it
                                                    int64_t noised_len, const float* __restrict__ x,
                                                    const float* __restrict__ sigma,
                                                    const float* __restrict__ host_noise, uint32_t k0, uint32_t k1,
-                                                   int64_t sample_base, float* __restrict__ out) {
+                                                   int64_t sample_base, int64_t item_base,
+                                                   float* __restrict__ out) {
   const int64_t groups = (item_stride + 3) / 4;
   const int64_t total = n_samples * items * groups;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
@@ -89,7 +90,7 @@ __global__ void __launch_bounds__(256) k_noise_add(int64_t n_samples, int64_t it
     int64_t i = q % items;
     int64_t s = q / items;
     float z[4] = {0.f, 0.f, 0.f, 0.f};
-    if (!host_noise && 4 * g < noised_len) wam_normal4(g, i, sample_base + s, k0, k1, z);
+    if (!host_noise && 4 * g < noised_len) wam_normal4(g, item_base + i, sample_base + s, k0, k1, z);
     const float sg = host_noise ? 0.f : sigma[i];
     const float* xi = x + i * item_stride;
     float* oi = out + (s * items + i) * item_stride;
@@ -457,10 +458,10 @@ int wam_item_sigma(int64_t items, int64_t item_stride, int64_t len, const float*
   return WAM_OK;
 }
 
-int wam_noise_add(int64_t n_samples, int64_t items, int64_t item_stride, int64_t noised_len, const float* x,
-                  const float* sigma, const float* host_noise, uint64_t seed, int64_t sample_base, float* out,
-                  void* stream) {
-  if (n_samples < 0 || items < 0 || item_stride < 1 || noised_len < 0 || noised_len > item_stride || !x || !out)
+int wam_noise_add_ex(int64_t n_samples, int64_t items, int64_t item_stride, int64_t noised_len, const float* x,
+                     const float* sigma, const float* host_noise, uint64_t seed, int64_t sample_base,
+                     int64_t item_base, float* out, void* stream) {
+  if (item_base < 0 || n_samples < 0 || items < 0 || item_stride < 1 || noised_len < 0 || noised_len > item_stride || !x || !out)
     return WAM_ERR_INVALID_ARG;
   if (!host_noise && !sigma) return WAM_ERR_INVALID_ARG;
   int64_t work = n_samples * items * ((item_stride + 3) / 4);
@@ -471,13 +472,20 @@ int wam_noise_add(int64_t n_samples, int64_t items, int64_t item_stride, int64_t
       (!host_noise || (uintptr_t)host_noise % 16 == 0))
     hipLaunchKernelGGL(k_noise_add<true>, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, n_samples,
                        items, item_stride, noised_len, x, sigma, host_noise, (uint32_t)seed, (uint32_t)(seed >> 32),
-                       sample_base, out);
+                       sample_base, item_base, out);
   else
     hipLaunchKernelGGL(k_noise_add<false>, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, n_samples,
                        items, item_stride, noised_len, x, sigma, host_noise, (uint32_t)seed, (uint32_t)(seed >> 32),
-                       sample_base, out);
+                       sample_base, item_base, out);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
+}
+
+int wam_noise_add(int64_t n_samples, int64_t items, int64_t item_stride, int64_t noised_len, const float* x,
+                  const float* sigma, const float* host_noise, uint64_t seed, int64_t sample_base, float* out,
+                  void* stream) {
+  return wam_noise_add_ex(n_samples, items, item_stride, noised_len, x, sigma, host_noise, seed, sample_base, 0, out,
+                          stream);
 }
 
 int wam_subband_maps(const wam_plan* p, int64_t groups, int64_t group_items, int channels, const float* coeff_grads,

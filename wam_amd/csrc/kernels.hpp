@@ -35,6 +35,7 @@ struct WamNoise {
   int channels;           // C
   uint32_t k0, k1;        // seed
   int64_t sample_base;
+  int64_t image_base;     // global index of image 0 (Philox counter word; batch-sharded ranks)
 };
 
 // plane-resident multi-level 2D analysis (dwt2_plane.hip): all levels of a plane in one workgroup

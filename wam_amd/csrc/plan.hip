@@ -18,7 +18,7 @@
 
 extern "C" {
 
-int wam_version(void) { return 1; }
+int wam_version(void) { return 2; }
 
 const char* wam_strerror(int status) {
   switch (status) {
@@ -417,14 +417,21 @@ int wam_plan_caps(const wam_plan* p) {
   return caps;
 }
 
-int wam_wavedec_noisy(const wam_plan* p, int64_t n_samples, int64_t images, int channels, const float* x,
-                      const float* sigma, uint64_t seed, int64_t sample_base, float* coeffs, void* ws, void* stream) {
-  if (!p || !x || !sigma || !coeffs || !ws || n_samples < 0 || images < 0 || channels < 1) return WAM_ERR_INVALID_ARG;
+int wam_wavedec_noisy_ex(const wam_plan* p, int64_t n_samples, int64_t images, int channels, const float* x,
+                         const float* sigma, uint64_t seed, int64_t sample_base, int64_t image_base, float* coeffs,
+                         void* ws, void* stream) {
+  if (!p || !x || !sigma || !coeffs || !ws || n_samples < 0 || images < 0 || channels < 1 || image_base < 0)
+    return WAM_ERR_INVALID_ARG;
   if (!(wam_plan_caps(p) & WAM_CAP_NOISY_WAVEDEC)) return WAM_ERR_UNSUPPORTED;
   const int64_t batch = n_samples * images * channels;
   if (batch == 0) return WAM_OK;
-  WamNoise nz{sigma, images, channels, (uint32_t)seed, (uint32_t)(seed >> 32), sample_base};
+  WamNoise nz{sigma, images, channels, (uint32_t)seed, (uint32_t)(seed >> 32), sample_base, image_base};
   return analysis_driver(p, batch, x, coeffs, ws, (hipStream_t)stream, false, &nz, n_samples);
+}
+
+int wam_wavedec_noisy(const wam_plan* p, int64_t n_samples, int64_t images, int channels, const float* x,
+                      const float* sigma, uint64_t seed, int64_t sample_base, float* coeffs, void* ws, void* stream) {
+  return wam_wavedec_noisy_ex(p, n_samples, images, channels, x, sigma, seed, sample_base, 0, coeffs, ws, stream);
 }
 
 int wam_waverec_adjoint_maps(const wam_plan* p, int64_t groups, int64_t group_items, int channels, const float* grad,

@@ -37,29 +37,28 @@ def _is_int_label(y):
     return isinstance(y, (int, np.integer)) or (isinstance(y, torch.Tensor) and y.dim() == 0)
 
 
-def seed_gradient(out, y, groups, n, unit=False):
+def seed_gradient(out, y, groups, n, unit=False, batch=None):
     """d loss / d out for `groups` stacked reference calls of n items each.
+    batch = (first, total): the n items are items [first, first + n) of a reference batch of
+    `total` items (a batch-sharded rank); the loss scale and y's indexing follow the whole batch.
     unit=True: the seed holds 1.0 where the loss gradient is non-zero and the loss scale (1/N^2,
     1/N or 1/k) is returned beside it, so a low-precision model output (bf16) does not round the
     scale -- the caller applies it to the fp32 input gradient. Returns (seed, scale or None)."""
+    first, total = (0, n) if batch is None else batch
     go = torch.zeros_like(out, dtype=torch.float32)
     rows = torch.arange(groups * n, device=out.device)
     if _is_int_label(y):
-        val = torch.tensor(1.0, dtype=torch.float32) / (n * n)
+        val = torch.tensor(1.0, dtype=torch.float32) / (total * total)
         rr, cc = rows, torch.full((groups * n,), int(y), dtype=torch.long, device=out.device)
     else:
         yy = torch.as_tensor(np.asarray([int(v) for v in (y.tolist() if isinstance(y, torch.Tensor) else y)]),
                              dtype=torch.long)
-        if yy.numel() != n:
-            # the reference's diag(output[:, y]) with len(y) != N takes min(N, len(y)) entries
-            k = min(n, yy.numel())
-            val = torch.tensor(1.0, dtype=torch.float32) / k
-            sel = torch.arange(k)
-            rr = (torch.arange(groups)[:, None] * n + sel[None, :]).reshape(-1).to(out.device)
-            cc = yy[:k].repeat(groups).to(out.device)
-        else:
-            val = torch.tensor(1.0, dtype=torch.float32) / n
-            rr, cc = rows, yy.repeat(groups).to(out.device)
+        # the reference's diag(output[:, y]) takes min(N, len(y)) entries (all N when len(y) == N)
+        k = min(total, yy.numel())
+        val = torch.tensor(1.0, dtype=torch.float32) / k
+        sel = torch.arange(n)[first + torch.arange(n) < k]       # local items with a diagonal entry
+        rr = (torch.arange(groups)[:, None] * n + sel[None, :]).reshape(-1).to(out.device)
+        cc = yy[first + sel].repeat(groups).to(out.device)
     if unit:
         go[rr, cc] = 1.0
         return go.to(out.dtype), float(val)
@@ -68,7 +67,7 @@ def seed_gradient(out, y, groups, n, unit=False):
 
 
 def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=False, y_none_mean=False,
-                   input_dtype=None):
+                   input_dtype=None, batch=None):
     """Gradient of the summed per-group reference losses w.r.t. img (fp32)."""
     img = img.detach().requires_grad_(True)
     inp = img if input_dtype is None else img.to(input_dtype)
@@ -80,7 +79,7 @@ def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=
         loss = out.float().mean()
         (g,) = torch.autograd.grad(loss, img)
     else:
-        seed, scale = seed_gradient(out, y, groups, n, unit=out.dtype != torch.float32)
+        seed, scale = seed_gradient(out, y, groups, n, unit=out.dtype != torch.float32, batch=batch)
         (g,) = torch.autograd.grad(out, img, grad_outputs=seed)
         if scale is not None:
             g = g * scale
@@ -111,12 +110,13 @@ class GradModel:
                 self._run = self.model
         return self._run
 
-    def __call__(self, img, y, groups, n, y_none_mean=False):
+    def __call__(self, img, y, groups, n, y_none_mean=False, batch=None):
         run = self._runner()
         if self.optimize:
             return input_gradient(run, img, y, groups, n, None, self.channels_last, y_none_mean,
-                                  input_dtype=self.autocast_dtype)
-        return input_gradient(run, img, y, groups, n, self.autocast_dtype, self.channels_last, y_none_mean)
+                                  input_dtype=self.autocast_dtype, batch=batch)
+        return input_gradient(run, img, y, groups, n, self.autocast_dtype, self.channels_last, y_none_mean,
+                              batch=batch)
 
 
 def legacy_noise(sigmas, item_shape, seed, samples, n_total=None):
@@ -152,9 +152,7 @@ class Shard:
 
     def range(self, n):
         """Contiguous block of [0, n) for this rank (ragged: the first n % world ranks get one more)."""
-        q, r = divmod(n, self.world)
-        start = self.rank * q + min(self.rank, r)
-        return start, start + q + (1 if self.rank < r else 0)
+        return Shard.range_of(self.rank, self.world, n)
 
     def all_reduce_sum(self, t):
         if self.world > 1:
@@ -165,6 +163,28 @@ class Shard:
         if self.world > 1:
             tdist.all_reduce(t, op=tdist.ReduceOp.MAX, group=self.group)
         return t
+
+    def all_gather_rows(self, t, n):
+        """t: this rank's rows [range(n)] of an [n, ...] tensor -> the whole tensor on every rank
+        (ragged ranges padded to the longest for the collective)."""
+        if self.world == 1:
+            return t
+        q = -(-n // self.world)
+        pad = t.new_zeros((q,) + tuple(t.shape[1:]))
+        pad[:t.shape[0]] = t
+        parts = [torch.empty_like(pad) for _ in range(self.world)]
+        tdist.all_gather(parts, pad, group=self.group)
+        out = []
+        for r in range(self.world):
+            lo, hi = Shard.range_of(r, self.world, n)
+            out.append(parts[r][:hi - lo])
+        return torch.cat(out)
+
+    @staticmethod
+    def range_of(rank, world, n):
+        q, r = divmod(n, world)
+        start = rank * q + min(rank, r)
+        return start, start + q + (1 if rank < r else 0)
 
 
 def ig_weights(k0, cnt, n):

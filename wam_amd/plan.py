@@ -125,17 +125,18 @@ class Plan:
     def caps(self):
         return lib.wam_plan_caps(self._h)
 
-    def wavedec_noisy(self, x, sigma, n_samples, images, channels, seed, sample_base=0, out=None):
-        """coefficients of x + sigma_i N(0,1) (Philox) for n_samples x images x channels planes."""
+    def wavedec_noisy(self, x, sigma, n_samples, images, channels, seed, sample_base=0, out=None, image_base=0):
+        """coefficients of x + sigma_i N(0,1) (Philox) for n_samples x images x channels planes;
+        image_base = global index of x's first image (Philox counter of a batch-sharded rank)."""
         require_cuda(x, "x")
         x = x.contiguous()
         batch = n_samples * images * channels
         if out is None:
             out = torch.empty(batch * self.coeff_numel, dtype=torch.float32, device=x.device)
         ws = self.workspace(batch)
-        check(lib.wam_wavedec_noisy(self._h, n_samples, images, channels, ptr(x), ptr(sigma),
-                                    ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), sample_base, ptr(out), ptr(ws),
-                                    stream_of(x.device)))
+        check(lib.wam_wavedec_noisy_ex(self._h, n_samples, images, channels, ptr(x), ptr(sigma),
+                                       ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), sample_base, image_base, ptr(out),
+                                       ptr(ws), stream_of(x.device)))
         return out
 
     def adjoint_maps(self, grad, groups, group_items, channels, full=False):
@@ -204,12 +205,13 @@ def item_sigma(x, item_stride, length, spread):
     return sigma
 
 
-def noise_add(x, sigma, n_samples, items, item_stride, noised_len, seed=0, sample_base=0, host_noise=None, out=None):
+def noise_add(x, sigma, n_samples, items, item_stride, noised_len, seed=0, sample_base=0, host_noise=None, out=None,
+              item_base=0):
     if out is None:
         out = torch.empty((n_samples * items * item_stride,), dtype=torch.float32, device=x.device)
-    check(lib.wam_noise_add(n_samples, items, item_stride, noised_len, ptr(x), ptr(sigma), ptr(host_noise),
-                            ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), sample_base, ptr(out),
-                            stream_of(x.device)))
+    check(lib.wam_noise_add_ex(n_samples, items, item_stride, noised_len, ptr(x), ptr(sigma), ptr(host_noise),
+                               ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), sample_base, item_base, ptr(out),
+                               stream_of(x.device)))
     return out
 
 

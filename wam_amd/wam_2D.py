@@ -18,8 +18,13 @@ Build-only keyword arguments (all optional, after the reference's own):
   optimize_model run an eval-mode model as a traced copy with BatchNorm folded into the convs, a
                  polyphase input-gradient for the stride-2 input conv and weights cast once to
                  autocast_dtype (wam_amd/model_opt.py); same function up to fp rounding.
-  dist           True / ProcessGroup: shard samples (steps) over torch.distributed ranks and
-                 all-reduce the accumulated map (RCCL on ROCm); every rank returns the full map.
+  dist           True / ProcessGroup: shard the work over torch.distributed ranks (RCCL on ROCm);
+                 every rank returns the full map.
+  dist_axis      'samples' = noise samples / IG steps in contiguous ranges, partial maps summed by
+                 one all-reduce; 'images' = the input batch in contiguous ranges, the per-sample
+                 batch-global band maxima combined by an all-reduce MAX before normalising and the
+                 rows gathered at the end; 'auto' (default) = 'images' when every rank gets an
+                 image, else 'samples'.
 """
 import numpy as np
 import torch
@@ -286,7 +291,7 @@ class WaveletAttribution2D(BaseWAM2D):
     def __init__(self, model, wavelet="haar", method="smooth", J=3, device=None, mode="reflect", approx_coeffs=False,
                  normalize_coeffs=True, n_samples=25, stdev_spread=0.25, random_seed=42, *, noise="numpy",
                  frame="legacy", sample_batch=None, autocast_dtype=None, channels_last=False, dist=None,
-                 optimize_model=False):
+                 optimize_model=False, dist_axis="auto"):
         super().__init__(model, wavelet=wavelet, J=J, device=device, mode=mode, approx_coeffs=approx_coeffs,
                          normalize_coeffs=normalize_coeffs, frame=frame, autocast_dtype=autocast_dtype,
                          channels_last=channels_last, optimize_model=optimize_model)
@@ -299,6 +304,9 @@ class WaveletAttribution2D(BaseWAM2D):
         self.noise = noise
         self.sample_batch = sample_batch
         self.dist = dist
+        if dist_axis not in ("auto", "samples", "images"):
+            raise ValueError("dist_axis must be 'auto', 'samples' or 'images'")
+        self.dist_axis = dist_axis
         self.wam = BaseWAM2D(model, wavelet=wavelet, J=J, mode=mode, device=device, approx_coeffs=approx_coeffs,
                              normalize_coeffs=normalize_coeffs, frame=frame, autocast_dtype=autocast_dtype,
                              channels_last=channels_last, _grad=self._grad)
@@ -324,57 +332,80 @@ class WaveletAttribution2D(BaseWAM2D):
         per_sample = 4 * n * (c * plan.coeff_numel + 2 * c * int(np.prod(plan.rec_shape)) + plan.coeff_numel)
         return wam_group(model_group, total, per_sample)
 
-    def _gradients(self, imgs, y, groups, n, model_group):
-        """Input gradients of `groups` stacked reference calls, model run `model_group` at a time."""
+    def _gradients(self, imgs, y, groups, n, model_group, batch=None):
+        """Input gradients of `groups` stacked reference calls, model run `model_group` at a time;
+        batch = (first, total) when the n images are a rank's slice of the reference batch."""
         if groups <= model_group:
-            return self._grad(imgs, y, groups, n)
+            return self._grad(imgs, y, groups, n, batch=batch)
         out = torch.empty_like(imgs)
         for s0, cnt in chunks(0, groups, model_group):
-            out[s0 * n:(s0 + cnt) * n] = self._grad(imgs[s0 * n:(s0 + cnt) * n], y, cnt, n)
+            out[s0 * n:(s0 + cnt) * n] = self._grad(imgs[s0 * n:(s0 + cnt) * n], y, cnt, n, batch=batch)
         return out
+
+    def _split(self, n, n_steps):
+        """(shard, axis, image range, sample/step range) of this rank."""
+        shard = Shard(self.dist)
+        axis = self.dist_axis
+        if axis == "auto":
+            axis = "images" if n >= shard.world else "samples"
+        if shard.world == 1:
+            axis = "samples"
+        if axis == "images" and n < shard.world:
+            raise ValueError("dist_axis='images' needs at least one image per rank (%d images, %d ranks)"
+                             % (n, shard.world))
+        if axis == "images":
+            return shard, axis, shard.range(n), (0, n_steps)
+        return shard, axis, (0, n), shard.range(n_steps)
 
     def smooth_gradcam(self, x, y):
         """lib/wam_2D.py:379-415."""
         dev = self._dev
         x = self._prep(x)
-        n, c, h, w = x.shape
+        N, c, h, w = x.shape
         plan = get_plan(2, (h, w), self.J, self.wavelet, self.mode, dev)
-        gmap, (rh, rw) = frames.smooth_frame(plan, n, self.frame, dev)
         item = c * h * w
-        sigma = item_sigma(x, item, item, self.stdev_spread)
-        shard = Shard(self.dist)
-        s_lo, s_hi = shard.range(self.n_samples)
+        sigma_all = item_sigma(x, item, item, self.stdev_spread)
+        shard, axis, (i_lo, i_hi), (s_lo, s_hi) = self._split(N, self.n_samples)
+        n = i_hi - i_lo                      # this rank's images
+        xs, sigma = x[i_lo:i_hi], sigma_all[i_lo:i_hi]
+        batch = (i_lo, N) if axis == "images" else None
+        gmap, (rh, rw) = frames.smooth_frame(plan, n, self.frame, dev)
         group = auto_group(self.model, n, self.sample_batch)
         # parity mode streams the host-generated legacy noise one model group at a time
         wgroup = group if self.noise == "numpy" else self._wam_group(plan, n, c, group, s_hi - s_lo)
         frame = torch.zeros(n * rh * rw, dtype=torch.float64, device=dev)
         noise_it = None
         if self.noise == "numpy":
-            noise_it = legacy_noise([float(v) for v in sigma.cpu().numpy()], (c, h, w), self.random_seed,
+            noise_it = legacy_noise([float(v) for v in sigma_all.cpu().numpy()], (c, h, w), self.random_seed,
                                     list(range(s_lo, s_hi)))
         rec = plan.rec_shape
         last = None
         for s0, cnt in chunks(s_lo, s_hi, wgroup):
             if noise_it is not None:
-                arr = np.stack([next(noise_it)[1] for _ in range(cnt)])
+                arr = np.stack([next(noise_it)[1][i_lo:i_hi] for _ in range(cnt)])
                 host = torch.from_numpy(arr).pin_memory().to(dev, non_blocking=True)
-                noisy = noise_add(x, sigma, cnt, n, item, item, host_noise=host)
+                noisy = noise_add(xs, sigma, cnt, n, item, item, host_noise=host)
                 flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
-            elif plan.caps & CAP_NOISY_WAVEDEC:
-                flat = plan.wavedec_noisy(x, sigma, cnt, n, c, self.random_seed, s0)  # noise fused on the load
+            elif plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
+                flat = plan.wavedec_noisy(xs, sigma, cnt, n, c, self.random_seed, s0, image_base=i_lo)
             else:
-                noisy = noise_add(x, sigma, cnt, n, item, item, seed=self.random_seed, sample_base=s0)
+                noisy = noise_add(xs, sigma, cnt, n, item, item, seed=self.random_seed, sample_base=s0, item_base=i_lo)
                 flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
             img = plan.waverec(flat, cnt * n * c)[0].view((cnt * n, c) + rec)
-            g = self._gradients(img, y, cnt, n, group)
+            g = self._gradients(img, y, cnt, n, group, batch)
             maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
+            if axis == "images":
+                shard.all_reduce_max(bmax)  # per-sample maxima over the whole batch (A.6)
             frame_accumulate(cnt, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, frame)
             last = (plan, flat, None, cnt * n * c, (cnt - 1) * n, n, c)
             last_g = g[(cnt - 1) * n:].reshape((n * c,) + rec)
         if last is not None:
             self.wam._record_pass(*last, grad_img=last_g)
-        shard.all_reduce_sum(frame)
-        avg = frame.view(n, rh, rw) / self.n_samples
+        if axis == "images":
+            frame = shard.all_gather_rows(frame.view(n, rh * rw), N).reshape(-1)
+        else:
+            shard.all_reduce_sum(frame)
+        avg = frame.view(N, rh, rw) / self.n_samples
         self._set_result(avg)
         return avg.cpu().numpy()
 
@@ -382,16 +413,19 @@ class WaveletAttribution2D(BaseWAM2D):
         """lib/wam_2D.py:417-459 (trapezoid over alpha = linspace(0, 1, n_samples), dx = 1)."""
         dev = self._dev
         x = self._prep(x)
-        n, c, h, w = x.shape
+        N, c, h, w = x.shape
         plan = get_plan(2, (h, w), self.J, self.wavelet, self.mode, dev)
+        shard, axis, (i_lo, i_hi), (k_lo, k_hi) = self._split(N, self.n_samples)
+        n = i_hi - i_lo
+        batch = (i_lo, N) if axis == "images" else None
         bmap, gmap, (rh, rw) = frames.ig_frames(plan, n, self.frame, dev)
-        z = plan.wavedec(x.view(n * c, h, w))
+        z = plan.wavedec(x[i_lo:i_hi].reshape(n * c, h, w))
         zmaps, zmax = subband_maps(plan, z, 1, n, c)
+        if axis == "images":
+            shard.all_reduce_max(zmax)
         base = torch.zeros(n * rh * rw, dtype=torch.float64, device=dev)
         frame_accumulate(1, n, bmap, zmaps, plan.coeff_numel, zmax, plan.nbands, True, base)
         alphas = np.linspace(0, 1, self.n_samples)
-        shard = Shard(self.dist)
-        k_lo, k_hi = shard.range(self.n_samples)
         group = auto_group(self.model, n, self.sample_batch)
         wgroup = self._wam_group(plan, n, c, group, k_hi - k_lo)
         acc = torch.zeros(n * rh * rw, dtype=torch.float32, device=dev)
@@ -400,10 +434,12 @@ class WaveletAttribution2D(BaseWAM2D):
         last = None
         for k0, cnt in chunks(k_lo, k_hi, wgroup):
             img = plan.waverec(z, n * c, alphas=alphas[k0:k0 + cnt]).view((cnt * n, c) + rec)
-            g = self._gradients(img, y, cnt, n, group)
+            g = self._gradients(img, y, cnt, n, group, batch)
             maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
+            if axis == "images":
+                shard.all_reduce_max(bmax)
             weights = None
-            if shard.world > 1:
+            if axis == "samples" and shard.world > 1:
                 weights = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
             frame_trapz(cnt, k0, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, prev, acc,
                         weights)
@@ -413,8 +449,12 @@ class WaveletAttribution2D(BaseWAM2D):
             plan_, alpha = last
             coeff = z * float(np.float32(alpha))  # the path coefficients alpha * z of the last step
             self.wam._record_pass(plan_, coeff, None, n * c, 0, n, c, grad_img=last_g)
-        shard.all_reduce_sum(acc)
-        out = base.view(n, rh, rw) * acc.view(n, rh, rw).double()
+        if axis == "images":
+            base = shard.all_gather_rows(base.view(n, rh * rw), N)
+            acc = shard.all_gather_rows(acc.view(n, rh * rw), N)
+        else:
+            shard.all_reduce_sum(acc)
+        out = base.view(N, rh, rw) * acc.view(N, rh, rw).double()
         self._set_result(out)
         return out.cpu().numpy()
 
