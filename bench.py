@@ -1,35 +1,51 @@
-"""WAM-2D throughput bench on MI355X (the BASELINE.json metric).
+"""WAM attribution throughput bench on MI355X (the BASELINE.json metric and its five configs).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--config c2] [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-Workload (BASELINE.json configs[1], the metric's config): WAM-2D SmoothGrad, db4, J=3,
-n_samples=25, batch 64 of synthetic 224x224 images (RandomState(1) N(0,1), ImageNet-normalised
-scale), labels RandomState(2).randint(0, 1000, 64) as a list, random-init ResNet-50 (no network:
-synthetic data, random weights). One STEP = one explainer call on the 64-image batch = 64
-attributions, 1600 model forward/backward passes. The reference cannot run db4 SmoothGrad at 224
-(its hard-coded 224 canvas vs a 230 mosaic); the native frame (E1: crop to the
-input size) is used, identical to the reference wherever the reference runs.
-Multi-GPU: one process per GPU, each rank explains its own 64-image batch (independent
-attributions, no data-path collective) -> "scaling": "weak"; value = all ranks' attributions /
-max-over-ranks time.
+Workloads (BASELINE.json `configs`; synthetic data, random-init weights -- no
+network). One STEP = one explainer call on the config's whole batch:
+  c1  WAM-2D haar J=3 SmoothGrad n=25, ResNet-18 fp32, 1 image (the elephant crop fixture),
+      numpy noise, legacy frame: the reference's own CPU-runnable case (CPU cross-check).
+  c2  WAM-2D db4 J=3 SmoothGrad n=25, ResNet-50 (bf16, BN folded), batch 64 of 224^2, Philox
+      noise, native frame E1 (the reference cannot run db4 SmoothGrad at 224).
+      THE metric's config and the default.
+  c3  WAM-1D db6 J=5 SmoothGrad n=25, FtEx audio CNN (bf16 autocast) on the mel front-end,
+      batch 256 clips of 5 s at 16 kHz, Philox noise.
+  c4  WAM-2D sym8 J=5 Integrated Gradients, 64 path steps, ResNet-50 (bf16, BN folded), batch
+      128 of 512^2, native frame E2.
+  c5  WAM-3D haar J=2 SmoothGrad n=25 (symmetric), Voxel3D CNN (bf16 autocast), batch 16 of 128^3,
+      Philox noise, legacy in-loop averaging.
+Multi-GPU (one process per GPU, RCCL): the explainer itself shards ONE call of the batch with
+dist=True -- c2/c4 over the batch (each rank a contiguous image range, the per-sample
+batch-global maxima combined by an all-reduce MAX, the rows gathered), c3/c5 over the noise
+samples (partial accumulators summed by an all-reduce) -- so "scaling" is "strong" and value =
+the call's attributions / max-over-ranks time. N > 1 also reports the collectives' time and a
+weak-scaling figure (each rank its own batch, no collective) as secondary fields.
 
 The JSON line also carries
-  roofline      the dominant WAM transform (largest total time) measured live with HIP events on
-                the stream the kernels run on: SURVEY 8(d) algorithmic bytes per launch (4 (P+K)
-                per image-sample x image-samples per launch) / mean launch time vs the 8 TB/s HBM
-                peak; fused_min_* = the fused kernel's own minimum bytes (clean input read once);
-                traffic = PMC HBM bytes per launch from profiles/*_pmc.json when a matching
-                rocprofv3 --pmc capture is committed (else null);
+  roofline      the dominant WAM kernel (largest total time), timed live with HIP events that
+                libwam_hip.so records on the launch stream: SURVEY 8(d) algorithmic bytes per
+                launch / mean launch time vs the 8 TB/s HBM peak; traffic = HBM bytes per launch
+                from rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes that this run
+                starts itself before it touches the GPU (one call of the same config with a stand-in
+                model, so the WAM kernels see the same shapes), else null;
   cpu_baseline  the reference algorithm (oracle/wam_ref.py: per-sample loop, torch-CPU ptwt
-                restatement, numpy legacy noise, numpy mosaic; fp32 ResNet-50) on a bounded
-                sample on the host cores, rank 0 at N=1 only.
+                restatement, numpy legacy noise, numpy mosaic; fp32 model) on a bounded sample on
+                the host cores, rank 0 at N=1 only;
+  c2 extras     parity (GPU fp32 map vs that CPU reference map on the same images; bf16 + folded
+                model vs fp32; Philox vs numpy noise), variant throughputs (fp32 model, model run
+                as is under autocast), DWT->IDWT round-trip error, a measured copy ceiling.
 """
 import argparse
+import csv
 import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -40,114 +56,216 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0
-N_IMAGES = 64
-N_SAMPLES = 25
+
+
+# ============================================================================ configurations
+class Workload:
+    """One BASELINE config: inputs, model, explainer kwargs, units and algorithmic bytes."""
+
+    def __init__(self, name, dim, metric, unit, n, n_steps, make_x, make_y, model, kw, model_dtype,
+                 describe, dist_axis):
+        self.name, self.dim, self.metric, self.unit = name, dim, metric, unit
+        self.n, self.n_steps = n, n_steps          # batch items, noise samples / IG steps per item
+        self.make_x, self.make_y, self.model, self.kw = make_x, make_y, model, kw
+        self.model_dtype, self.describe, self.dist_axis = model_dtype, describe, dist_axis
+
+
+def _clips(n, length=80000, sr=16000, seed=3):
+    """SURVEY 8(d) c3 input: 3 random sinusoids (50-4000 Hz) + 0.1 N(0,1), peak-normalised."""
+    rs = np.random.RandomState(seed)
+    t = np.arange(length) / sr
+    out = np.empty((n, length), dtype=np.float32)
+    for i in range(n):
+        f = rs.uniform(50, 4000, 3)
+        a = rs.uniform(0.2, 1.0, 3)
+        w = (a[:, None] * np.sin(2 * np.pi * f[:, None] * t[None])).sum(0) + 0.1 * rs.standard_normal(length)
+        out[i] = (w / np.abs(w).max()).astype(np.float32)
+    return torch.tensor(out)
+
+
+def _volumes(n, size=128, seed=5):
+    """SURVEY 8(d) c5 input: Gaussian-smoothed N(0,1) thresholded to {0, 1}."""
+    g = torch.Generator().manual_seed(seed)
+    v = torch.randn(n, 1, size, size, size, generator=g)
+    k = torch.tensor([0.25, 0.5, 0.25])
+    for ax in (2, 3, 4):
+        shape = [1, 1, 1, 1, 1]
+        shape[ax] = 3
+        v = torch.nn.functional.conv3d(v, k.view(shape), padding=[1 if a == ax else 0 for a in (2, 3, 4)])
+    return (v > 0).float()
+
+
+def _elephant():
+    crop = np.load(os.path.join(REPO, "tests", "golden", "elephant_224.npz"))["crop"].astype(np.float32) / 255.0
+    mean = np.array([0.485, 0.456, 0.406], dtype=np.float32)[:, None, None]
+    std = np.array([0.229, 0.224, 0.225], dtype=np.float32)[:, None, None]
+    return torch.tensor(((crop.transpose(2, 0, 1) - mean) / std)[None])
+
+
+def workload(name):
+    import testmodels
+    if name == "c1":
+        return Workload("c1", 2, "WAM-2D attributions/sec @224^2 n_samples=25 (haar J=3 SmoothGrad, ResNet-18, 1 image)",
+                        "attributions/s", 1, 25, _elephant, None, lambda: testmodels.resnet18(seed=0),
+                        dict(wavelet="haar", J=3, method="smooth", mode="reflect", n_samples=25), "fp32",
+                        "c1: WAM-2D haar J=3 SmoothGrad n=25, ResNet-18 (random init), 1 image 224x224 (elephant "
+                        "crop), numpy legacy noise, legacy frame", "samples")
+    if name == "c2":
+        return Workload("c2", 2, "WAM-2D attributions/sec @224^2 n_samples=25 (db4 J=3 SmoothGrad, ResNet-50)",
+                        "attributions/s", 64, 25,
+                        lambda: torch.tensor(np.random.RandomState(1).standard_normal((64, 3, 224, 224))
+                                             .astype(np.float32)),
+                        lambda: [int(v) for v in np.random.RandomState(2).randint(0, 1000, 64)],
+                        lambda: testmodels.resnet50(seed=0),
+                        dict(wavelet="db4", J=3, method="smooth", mode="reflect", n_samples=25, noise="philox",
+                             frame="native"), "bf16",
+                        "c2: WAM-2D db4 J=3 SmoothGrad n_samples=25, batch 64 x 224x224, ResNet-50", "images")
+    if name == "c3":
+        return Workload("c3", 1, "WAM-1D attributions/sec, 5 s 16 kHz clips n_samples=25 (db6 J=5 SmoothGrad, FtEx)",
+                        "attributions/s", 256, 25, lambda: _clips(256),
+                        lambda: [int(v) for v in np.random.RandomState(6).randint(0, 50, 256)],
+                        lambda: testmodels.FtEx(seed=0),
+                        dict(wavelet="db6", J=5, method="smooth", mode="reflect", n_samples=25, sample_rate=16000,
+                             noise="philox"), "bf16",
+                        "c3: WAM-1D db6 J=5 SmoothGrad n_samples=25, batch 256 x 80000 samples, FtEx audio CNN",
+                        "samples")
+    if name == "c4":
+        return Workload("c4", 2, "WAM-2D attributions/sec @512^2 (sym8 J=5 Integrated Gradients, 64 steps, ResNet-50)",
+                        "attributions/s", 128, 64,
+                        lambda: torch.tensor(np.random.RandomState(4).standard_normal((128, 3, 512, 512))
+                                             .astype(np.float32)),
+                        lambda: [int(v) for v in np.random.RandomState(7).randint(0, 1000, 128)],
+                        lambda: testmodels.resnet50(seed=0),
+                        dict(wavelet="sym8", J=5, method="integratedgrad", mode="reflect", n_samples=64,
+                             frame="native"), "bf16",
+                        "c4: WAM-2D sym8 J=5 Integrated Gradients (64 path steps), batch 128 x 512x512, ResNet-50",
+                        "images")
+    if name == "c5":
+        return Workload("c5", 3, "WAM-3D attributions/sec @128^3 n_samples=25 (haar J=2 SmoothGrad, Voxel3D)",
+                        "attributions/s", 16, 25, lambda: _volumes(16),
+                        lambda: [int(v) for v in np.random.RandomState(8).randint(0, 10, 16)],
+                        lambda: testmodels.Voxel3D(seed=0),
+                        dict(wavelet="haar", J=2, method="smooth", mode="symmetric", n_samples=25,
+                             noise="philox"), "bf16",
+                        "c5: WAM-3D haar J=2 SmoothGrad n_samples=25, batch 16 x 128^3, Voxel3D CNN", "samples")
+    raise ValueError(name)
 
 
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--model-dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--sample-batch", type=int, default=13, help="noise samples per model call (x64 images)")
-    ap.add_argument("--channels-last", dest="channels_last", action="store_true", default=True,
-                    help="NHWC model execution (default; faster than NCHW for the BN-folded bf16 model)")
-    ap.add_argument("--no-channels-last", dest="channels_last", action="store_false")
+    ap.add_argument("--model-dtype", default=None, choices=["bf16", "fp32"], help="default: the config's")
+    ap.add_argument("--sample-batch", type=int, default=None,
+                    help="noise samples / IG steps per model call (default: ~832 images per call for c2/c4)")
     ap.add_argument("--no-optimize-model", action="store_true",
-                    help="run the model as is under autocast instead of the BN-folded bf16 copy (model_opt.py)")
+                    help="run the model as is under autocast instead of the BN-folded copy (model_opt.py)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--pmc", default="auto", choices=["auto", "off"])
+    ap.add_argument("--extras", default="auto", choices=["auto", "off"], help="c2 parity / variants / ceilings")
+    ap.add_argument("--dist-axis", default=None, choices=["auto", "samples", "images"])
+    ap.add_argument("--wam-probe", action="store_true", help=argparse.SUPPRESS)  # PMC child run
     return ap.parse_args()
 
 
-def make_inputs():
-    x = torch.tensor(np.random.RandomState(1).standard_normal((N_IMAGES, 3, 224, 224)).astype(np.float32))
-    y = [int(v) for v in np.random.RandomState(2).randint(0, 1000, N_IMAGES)]
-    return x, y
-
-
-def cpu_baseline(seconds):
-    """Reference algorithm on the host cores, bounded sample (images x noise samples)."""
-    import testmodels
-    from oracle import wam_ref
-    cores = len(os.sched_getaffinity(0))
-    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
-    torch.set_num_threads(cores)
-    model = testmodels.resnet50(seed=0)
-    x, y = make_inputs()
-    # calibrate on one image x one sample, then size the sample to ~`seconds` of CPU work
-    for _ in range(2):  # the first call pays one-time CPU start-up costs
-        t0 = time.perf_counter()
-        wam_ref.smooth_2d(model, x[:2], y[:2], wavelet="db4", J=3, mode="reflect", n_samples=1, frame="native")
-        t1 = (time.perf_counter() - t0) / 2
-    per = max(t1, 1e-3)
-    # images x samples sized to ~`seconds` of CPU work: all 25 samples of as many images as fit
-    n_s = N_SAMPLES if seconds / per >= N_SAMPLES else int(max(1, seconds / per))
-    n_img = int(max(1, min(N_IMAGES, seconds / per / n_s)))
-    t0 = time.perf_counter()
-    wam_ref.smooth_2d(model, x[:n_img], y[:n_img], wavelet="db4", J=3, mode="reflect", n_samples=n_s, frame="native")
-    dt = time.perf_counter() - t0
-    image_samples_per_s = n_img * n_s / dt
-    cpu_model = "unknown CPU"
-    try:
-        with open("/proc/cpuinfo") as f:
-            cpu_model = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
-    except (OSError, StopIteration):
-        pass
-    return {"value": image_samples_per_s / N_SAMPLES, "unit": "attributions/s", "cores": cores,
-            "kind": "port",
-            "sample": "oracle/wam_ref.smooth_2d (reference glue restated on torch-CPU ptwt, numpy legacy noise), "
-                      "fp32 ResNet-50, %d image(s) x %d noise sample(s) of the c2 workload in %.1f s on %d "
-                      "thread(s) of %s, extrapolated to 25 samples per attribution" % (n_img, n_s, dt, cores,
-                                                                                       cpu_model)}
-
-
-def load_traffic(op_kernel):
-    """PMC HBM bytes per call of the dominant op from the newest committed profiles/*_pmc.json."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")))
-    if not files:
-        return None
-    try:
-        with open(files[-1]) as f:
-            d = json.load(f)
-        return d.get("per_call_bytes", {}).get(op_kernel)
-    except Exception:
-        return None
-
-
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
-    import testmodels
-    from wam_amd import plan as P
-    from wam_amd.wam_2D import WaveletAttribution2D
-
-    model = testmodels.resnet50(seed=0).to(dev)
-    if args.channels_last:
-        model = model.to(memory_format=torch.channels_last)
+# ============================================================================ explainer
+def build_explainer(wl, dev, args, model=None, dist_on=False, model_dtype=None, optimize=None, noise=None,
+                    n_local=None):
+    import wam_amd
+    model_dtype = model_dtype or args.model_dtype or wl.model_dtype
+    model = (model if model is not None else wl.model()).to(dev).eval()
     for p in model.parameters():
         p.requires_grad_(False)
-    x, y = make_inputs()
-    x = x.to(dev)
-    ex = WaveletAttribution2D(model, wavelet="db4", J=3, method="smooth", mode="reflect", n_samples=N_SAMPLES,
-                              noise="philox", frame="native", sample_batch=args.sample_batch,
-                              autocast_dtype=torch.bfloat16 if args.model_dtype == "bf16" else None,
-                              channels_last=args.channels_last, optimize_model=not args.no_optimize_model)
+    kw = dict(wl.kw)
+    if noise is not None:
+        kw["noise"] = noise
+    ac = torch.bfloat16 if model_dtype == "bf16" else None
+    if wl.dim == 2:
+        opt = (not args.no_optimize_model) if optimize is None else optimize
+        opt = opt and wl.name != "c1"
+        cl = wl.name != "c1"
+        if cl:
+            model = model.to(memory_format=torch.channels_last)
+        sb = args.sample_batch or _auto_sample_batch(wl, n_local or wl.n)
+        return wam_amd.WaveletAttribution2D(model, sample_batch=sb, autocast_dtype=ac, channels_last=cl,
+                                            optimize_model=opt, dist=True if dist_on else None,
+                                            dist_axis=args.dist_axis or wl.dist_axis, **kw)
+    if wl.dim == 1:
+        return wam_amd.WaveletAttribution1D(model, sample_batch=args.sample_batch or 5, autocast_dtype=ac,
+                                            dist=True if dist_on else None, **kw)
+    return wam_amd.WaveletAttribution3D(model, sample_batch=args.sample_batch or 2, autocast_dtype=ac,
+                                        dist=True if dist_on else None, **kw)
 
-    def step():
-        return ex(x, y)
 
-    for _ in range(args.warmup):
-        step()
+def _auto_sample_batch(wl, n_local):
+    """~832 images per model call (the measured sweet spot for ResNet-50 at 224^2; 512^2 images
+    count 5.2x), split evenly over the calls."""
+    per = 832 if wl.name != "c4" else 160
+    sb = max(1, min(wl.n_steps, -(-per // max(1, n_local))))
+    calls = -(-wl.n_steps // sb)
+    return -(-wl.n_steps // calls)
+
+
+# ============================================================================ timing helpers
+def kernel_table(records, steps):
+    kern = {}
+    for name, ms, nb in records:
+        k = kern.setdefault(name, {"launches": 0, "total_ms": 0.0, "bytes": 0.0})
+        k["launches"] += 1
+        k["total_ms"] += ms
+        k["bytes"] += nb
+    for k in kern.values():
+        k["mean_us"] = k["total_ms"] * 1e3 / k["launches"]
+        k["GBps"] = k["bytes"] / (k["total_ms"] * 1e-3) / 1e9 if k["total_ms"] > 0 else 0.0
+        k["bytes_per_launch"] = k["bytes"] / k["launches"]
+    return kern
+
+
+def unit_bytes(wl, kname, units_per_launch):
+    """SURVEY 8(d) algorithmic bytes of one launch where they differ from the library's own count
+    (the fused noisy analysis reads the clean input once for all its samples; 8(d) counts the
+    input of every (image x sample) unit, as the reference materialises each noisy image)."""
+    from wam_amd import plan as P
+    if wl.name != "c2":
+        return None
+    K = P.get_plan(2, (224, 224), 3, "db4", "reflect", "cuda").coeff_numel
+    per_unit = {"k_plane_ana<noise>": 4 * 3 * (224 * 224 + K),           # analysis 4 (P + K)
+                "k_plane_smooth": 4 * 3 * 2 * (224 * 224 + K),           # analysis + synthesis 2 x 4 (P + K)
+                "k_plane_syn": 4 * 3 * (K + 224 * 224),
+                "k_plane_maps": 4 * (3 * 224 * 224 + K)}.get(kname)
+    return None if per_unit is None else per_unit * units_per_launch
+
+
+def roofline(wl, kern, steps, units_per_step, traffic):
+    dom = max(kern, key=lambda n: kern[n]["total_ms"])
+    kd = kern[dom]
+    units_per_launch = units_per_step * steps / kd["launches"]
+    ub = unit_bytes(wl, dom, units_per_launch)
+    bpl = ub if ub else kd["bytes_per_launch"]
+    achieved = bpl / (kd["mean_us"] * 1e-6) / 1e9
+    tr = None
+    if traffic and dom in traffic.get("per_call_bytes", {}):
+        tr = traffic["per_call_bytes"][dom]
+    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr,
+            "traffic_per_launch_detail": (traffic or {}).get("per_call", {}).get(dom),
+            "traffic_source": (traffic or {}).get("source"),
+            "bytes_per_launch": round(bpl), "units_per_launch": units_per_launch,
+            "bytes_basis": "SURVEY 8(d) per (item x sample) unit" if ub else "library algorithmic bytes (4 (in + out))",
+            "library_bytes_per_launch": round(kd["bytes_per_launch"]), "library_GBps": round(kd["GBps"], 1),
+            "mean_us": round(kd["mean_us"], 2),
+            "wam_ms_per_step": round(sum(k["total_ms"] for k in kern.values()) / steps, 3),
+            "kernels": {n: {kk: round(vv, 3) for kk, vv in k.items()} for n, k in
+                        sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"])}}
+
+
+def timed(fn, steps, warmup, world, dev):
+    from wam_amd import plan as P
+    for _ in range(warmup):
+        fn()
     torch.cuda.synchronize(dev)
     P.timing_drain()
     P.timing_enable(True)
@@ -155,8 +273,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
+    out = None
+    for _ in range(steps):
+        out = fn()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -167,64 +286,347 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
-    assert out.shape == (N_IMAGES, 224, 224) and np.isfinite(out).all()
+    return dt, records, out
 
-    # live per-launch timing: HIP events recorded by libwam_hip.so around every launch, on the
-    # stream the kernel runs on; bytes = algorithmic (each input read once, each output written once)
-    kern = {}
-    for name, ms, nb in records:
-        k = kern.setdefault(name, {"launches": 0, "total_ms": 0.0, "bytes": 0.0})
-        k["launches"] += 1
-        k["total_ms"] += ms
-        k["bytes"] += nb
-    for k in kern.values():
-        k["mean_us"] = k["total_ms"] * 1e3 / k["launches"]
-        k["GBps"] = k["bytes"] / (k["total_ms"] * 1e-3) / 1e9
-        k["bytes_per_launch"] = k["bytes"] / k["launches"]
-    dom = max(kern, key=lambda n: kern[n]["total_ms"])
-    # achieved = SURVEY.md section 8(d)'s per-unit algorithmic bytes x the units one launch
-    # processes. The unit is one (image x noise sample); per unit the analysis moves 4 (P + K)
-    # bytes (P = C*H*W input values, K = C * coefficients per plane), the input of every sample
-    # counted as the reference materialises each noisy image. The fused noisy analysis reads the
-    # clean image once for all its samples, so it moves fewer bytes than that: its own minimum
-    # (clean input once + every sample's coefficients) is reported as fused_min_*.
-    kd = kern[dom]
-    units_per_launch = N_IMAGES * N_SAMPLES * args.steps / kd["launches"]
-    coeff_plane = P.get_plan(2, (224, 224), 3, "db4", "reflect", dev).coeff_numel
-    unit_bytes = {"k_plane_ana<noise>": 4 * 3 * (224 * 224 + coeff_plane),
-                  "k_plane_syn": 4 * 3 * (coeff_plane + 224 * 224),
-                  "k_plane_maps": 4 * (3 * 224 * 224 + coeff_plane)}.get(dom)
-    bpl = unit_bytes * units_per_launch if unit_bytes else kd["bytes_per_launch"]
-    achieved = bpl / (kd["mean_us"] * 1e-6) / 1e9
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(dom),
-                "bytes_per_launch": round(bpl), "units_per_launch": units_per_launch,
-                "bytes_basis": "SURVEY 8(d): 4(P+K) per image-sample" if unit_bytes else "library algorithmic bytes",
-                "fused_min_bytes_per_launch": round(kd["bytes_per_launch"]), "fused_min_GBps": round(kd["GBps"], 1),
-                "mean_us": round(kd["mean_us"], 2),
-                "wam_ms_per_step": round(sum(k["total_ms"] for k in kern.values()) / args.steps, 3),
-                "kernels": {n: {kk: round(vv, 3) for kk, vv in k.items()} for n, k in
-                            sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"])}}
 
-    cpu = None
+# ============================================================================ live PMC traffic
+def _short_kernel(name):
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    from pmc_summary import short
+    return short(name)
+
+
+def _pmc_pass(counter, config, outdir):
+    exe = shutil.which("rocprofv3")
+    cmd = ["timeout", "-s", "KILL", "150", exe, "--pmc", counter, "--kernel-include-regex", "k_[a-z0-9_]+",
+           "--output-format", "csv", "-d", outdir, "-o", "run", "--", sys.executable, os.path.join(REPO, "bench.py"),
+           "--config", config, "--wam-probe"]
+    env = dict(os.environ, TMPDIR="/tmp")
+    p = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=200)
+    files = glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True)
+    if p.returncode != 0 or not files:
+        raise RuntimeError("rocprofv3 --pmc %s failed (rc %d): %s" % (counter, p.returncode,
+                                                                       p.stdout.decode(errors="replace")[-600:]))
+    acc = {}
+    with open(files[0]) as f:
+        for row in csv.DictReader(f):
+            if row.get("Counter_Name") != counter:
+                continue
+            k = _short_kernel(row["Kernel_Name"])
+            if k is None:
+                continue
+            a = acc.setdefault(k, {})
+            d = row.get("Dispatch_Id") or row.get("Correlation_Id") or str(len(a))
+            a[d] = a.get(d, 0.0) + float(row["Counter_Value"]) * 1024.0  # KiB, summed over dimensions
+    return {k: (len(v), sum(v.values())) for k, v in acc.items()}
+
+
+def live_pmc(config):
+    """HBM traffic per WAM-kernel launch: two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; they
+    do not fit one pass) over one call of this config with a stand-in model, started before this
+    process touches the GPU. FETCH_SIZE is doubled (gfx950 counts 16-B-per-lane streaming reads at
+    half, MI355X_MICROARCH.md HBM section); WRITE_SIZE is taken as is."""
+    if not shutil.which("rocprofv3") or not shutil.which("timeout"):
+        return None
+    tmp = tempfile.mkdtemp(prefix="wam_pmc_", dir="/tmp")
+    try:
+        fetch = _pmc_pass("FETCH_SIZE", config, os.path.join(tmp, "f"))
+        write = _pmc_pass("WRITE_SIZE", config, os.path.join(tmp, "w"))
+    except Exception as e:  # profiler unavailable / refused: report null traffic, say why
+        return {"error": str(e)[:400]}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    out = {"source": "live rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and --pmc WRITE_SIZE passes over one %s call "
+                     "(stand-in model)" % config, "per_call_bytes": {}, "per_call": {}}
+    for k in sorted(set(fetch) | set(write)):
+        nf, bf = fetch.get(k, (0, 0.0))
+        nw, bw = write.get(k, (0, 0.0))
+        rd, wr = 2.0 * bf / max(nf, 1), bw / max(nw, 1)
+        out["per_call"][k] = {"launches": max(nf, nw), "read_bytes": round(rd), "write_bytes": round(wr)}
+        out["per_call_bytes"][k] = round(rd + wr)
+    return out
+
+
+class _StandIn(torch.nn.Module):
+    """Tiny model with the config's input/output shapes (PMC child runs: WAM kernels only)."""
+
+    def __init__(self, dim, n_classes):
+        super().__init__()
+        conv = {1: torch.nn.Conv2d, 2: torch.nn.Conv2d, 3: torch.nn.Conv3d}[dim]
+        self.conv = conv(1 if dim != 2 else 3, 4, 3, 2, 1)
+        self.fc = torch.nn.Linear(4, n_classes)
+
+    def forward(self, x):
+        h = torch.tanh(self.conv(x))
+        return self.fc(h.flatten(2).mean(-1))
+
+
+def wam_probe(args):
+    wl = workload(args.config)
+    dev = torch.device("cuda", 0)
+    x, y = wl.make_x(), (wl.make_y() if wl.make_y else 0)
+    model = _StandIn(wl.dim, 1000 if wl.dim == 2 else 50)
+    ex = build_explainer(wl, dev, args, model=model, model_dtype="fp32", optimize=False)
+    ex(x.to(dev), y)
+    torch.cuda.synchronize()
+
+
+# ============================================================================ CPU baseline
+def _cpu_threads():
+    cores = len(os.sched_getaffinity(0))
+    return min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+
+
+def _cpu_model_name():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except (OSError, StopIteration):
+        return "unknown CPU"
+
+
+def cpu_baseline(wl, seconds, x, y):
+    """The reference algorithm (oracle/wam_ref.py) on the host cores on a bounded sample of the
+    workload, extrapolated per attribution. Returns (record, (items, samples, cpu map) or None)."""
+    from oracle import wam_ref
+    cores = _cpu_threads()
+    torch.set_num_threads(cores)
+    model = wl.model().eval()
+    kw = {k: v for k, v in wl.kw.items() if k not in ("method", "noise", "n_samples")}
+    if wl.dim == 2:
+        fn = wam_ref.smooth_2d if wl.kw["method"] == "smooth" else wam_ref.ig_2d
+        if wl.kw["method"] != "smooth":
+            kw = {k: v for k, v in kw.items() if k in ("wavelet", "J", "mode", "frame")}
+    elif wl.dim == 1:
+        fn = wam_ref.smooth_1d
+    else:
+        fn = wam_ref.smooth_3d
+    run = lambda n_img, n_s: fn(model, x[:n_img], y[:n_img] if isinstance(y, list) else y, n_samples=n_s, **kw)
+    for _ in range(2):  # the first call pays one-time CPU start-up costs
+        t0 = time.perf_counter()
+        run(1, 1 if wl.kw["method"] == "smooth" else 2)
+        per = max(time.perf_counter() - t0, 1e-3)
+    if wl.kw["method"] != "smooth":
+        per /= 2
+    n_s = wl.n_steps if seconds / per >= wl.n_steps else int(max(2, seconds / per))
+    n_img = int(max(1, min(wl.n, seconds / per / n_s)))
+    t0 = time.perf_counter()
+    out = run(n_img, n_s)
+    dt = time.perf_counter() - t0
+    rec = {"value": n_img * n_s / dt / wl.n_steps, "unit": wl.unit, "cores": cores, "kind": "port",
+           "sample": "oracle/wam_ref (reference glue restated on torch-CPU ptwt, numpy legacy noise), fp32 model, "
+                     "%d item(s) x %d %s of the %s workload in %.1f s on %d thread(s) of %s%s" % (
+                         n_img, n_s, "noise samples" if wl.kw["method"] == "smooth" else "path steps", wl.name, dt,
+                         cores, _cpu_model_name(),
+                         "" if n_s == wl.n_steps else ", extrapolated to %d per attribution" % wl.n_steps)}
+    return rec, (n_img, n_s, out)
+
+
+# ============================================================================ c2 extras
+def _rel_l2(a, b):
+    return float(np.linalg.norm(a - b) / max(1e-30, np.linalg.norm(b)))
+
+
+def _top_iou(a, b, frac=0.10):
+    out = []
+    for u, v in zip(a.reshape(a.shape[0], -1), b.reshape(b.shape[0], -1)):
+        k = max(1, int(frac * u.size))
+        su, sv = set(np.argsort(-u)[:k].tolist()), set(np.argsort(-v)[:k].tolist())
+        out.append(len(su & sv) / len(su | sv))
+    return float(np.mean(out))
+
+
+def _cmp(a, b, what):
+    return {"what": what, "rel_l2": round(_rel_l2(a, b), 6), "max_abs": round(float(np.abs(a - b).max()), 6),
+            "top10_iou": round(_top_iou(a, b), 4), "items": int(a.shape[0])}
+
+
+def c2_extras(wl, dev, args, ex, x, y, cpu_ref):
+    """Parity numbers on the headline configuration, variant throughputs and ceilings."""
+    import wam_amd
+    from wam_amd import plan as P
+    extras = {}
+    n_sub = 8
+    xs, ys = x[:n_sub], y[:n_sub]
+    # the headline map (bf16, folded model, Philox) on the subset
+    head = ex(xs, ys)
+    fp32_philox = build_explainer(wl, dev, args, model_dtype="fp32", optimize=False)
+    b = fp32_philox(xs, ys)
+    fp32_numpy = build_explainer(wl, dev, args, model_dtype="fp32", optimize=False, noise="numpy")
+    c = fp32_numpy(xs, ys)
+    par = {"bf16_folded_vs_fp32": _cmp(head, b, "headline map (bf16, BN-folded model, Philox) vs fp32 model as is, "
+                                              "same Philox noise: model precision / folding only"),
+           "philox_vs_numpy_noise": _cmp(b, c, "fp32 model, Philox vs numpy legacy noise: Monte-Carlo spread of "
+                                              "two 25-sample SmoothGrad estimates (context, not an error)")}
+    if cpu_ref is not None:
+        n_img, n_s, ref = cpu_ref
+        ex_ref = build_explainer(wl, dev, args, model_dtype="fp32", optimize=False, noise="numpy")
+        ex_ref.n_samples = n_s
+        got = ex_ref(x[:n_img], y[:n_img])
+        par["gpu_fp32_vs_cpu_reference"] = _cmp(got, ref, "GPU (fp32 model, numpy noise) vs the CPU reference path "
+                                                          "(cpu_baseline's own output), same images / noise / "
+                                                          "weights; bar rel L2 <= 2e-2, max-abs <= 5e-2")
+        par["gpu_fp32_vs_cpu_reference"]["n_samples"] = n_s
+    extras["parity"] = par
+    del fp32_philox, fp32_numpy
+    torch.cuda.empty_cache()
+    # variant throughputs (short runs of the full call)
+    if args.extras == "auto":
+        var = {}
+        for tag, kw in (("fp32_model_folded", dict(model_dtype="fp32")),
+                        ("bf16_autocast_model_as_is", dict(model_dtype="bf16", optimize=False))):
+            e = build_explainer(wl, dev, args, **kw)
+            dt, _, _ = timed(lambda: e(x, y), 2, 1, 1, dev)
+            var[tag] = {"value": round(wl.n * 2 / dt, 3), "ms_per_step": round(dt / 2 * 1e3, 2), "steps": 2}
+            del e
+            torch.cuda.empty_cache()
+        extras["variants"] = var
+    # DWT -> IDWT round trip at the c2 geometry (north_star: "also reported")
+    p = P.get_plan(2, (224, 224), 3, "db4", "reflect", dev)
+    xd = x.to(dev).reshape(-1, 224, 224)
+    r = p.waverec(p.wavedec(xd), xd.shape[0])[0][:, :224, :224]
+    extras["roundtrip"] = {"max_abs": float((r - xd).abs().max()), "max_abs_input": float(xd.abs().max()),
+                           "what": "db4 J=3 reflect wavedec2 -> waverec2 of the 64x3 input planes (fp32)"}
+    # copy ceiling: device-to-device copy of 2 GiB
+    a = torch.empty(512 << 20, dtype=torch.float32, device=dev)
+    bb = torch.empty_like(a)
+    bb.copy_(a)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        bb.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / 10
+    extras["copy_ceiling"] = {"GBps": round(2 * a.numel() * 4 / (ms * 1e-3) / 1e9, 1), "bytes": 2 * a.numel() * 4,
+                              "what": "torch device copy of 2 GiB (read + write), mean of 10"}
+    del a, bb
+    return extras
+
+
+def collectives_timing(wl, dev, world, axis):
+    """The sharded call's collectives alone, at its sizes (20 reps after one warm-up)."""
+    from wam_amd import engine, plan as P
+    shard = engine.Shard(True)
+    ops = []
+    if axis == "images":
+        H = 224 if wl.name != "c4" else 512
+        nb = 3 * wl.kw["J"] + 1
+        lo, hi = shard.range(wl.n)
+        t = torch.rand(wl.n_steps, nb, device=dev)
+        rows = torch.zeros(hi - lo, H * H, dtype=torch.float64, device=dev)
+        ops.append(("all_reduce_max_band_maxima", lambda: shard.all_reduce_max(t)))
+        ops.append(("all_gather_frame_rows", lambda: shard.all_gather_rows(rows, wl.n)))
+    else:
+        if wl.dim == 1:
+            p = P.get_plan(1, (80000,), wl.kw["J"], wl.kw["wavelet"], wl.kw["mode"], dev)
+            numel = wl.n * (p.coeff_numel + (80000 // 512 + 1) * 128)
+            dt = torch.float32
+        elif wl.dim == 3:
+            numel, dt = wl.n * 128 ** 3, torch.float32
+        else:
+            numel, dt = wl.n * 224 * 224, torch.float64
+        acc = torch.zeros(numel, dtype=dt, device=dev)
+        ops.append(("all_reduce_sum_accumulators", lambda: shard.all_reduce_sum(acc)))
+    out = {}
+    for tag, fn in ops:
+        fn()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            fn()
+        torch.cuda.synchronize(dev)
+        out[tag + "_us"] = round((time.perf_counter() - t0) / 20 * 1e6, 1)
+    return out
+
+
+# ============================================================================ main
+def main():
+    args = parse()
+    if args.wam_probe:
+        return wam_probe(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    wl = workload(args.config)
+    traffic = None
+    if rank == 0 and world == 1 and args.pmc == "auto":
+        traffic = live_pmc(args.config)  # child processes, BEFORE this process touches the GPU
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    import wam_amd  # noqa: F401  (fails loudly without libwam_hip.so)
+    from wam_amd import engine
+
+    x, y = wl.make_x(), (wl.make_y() if wl.make_y else None)
+    if y is None:  # c1: the model's own top class (as the reference demo does)
+        with torch.no_grad():
+            y = int(wl.model()(x).argmax().item())
+    xd = x.to(dev)
+    shard_on = world > 1
+    axis = args.dist_axis or wl.dist_axis
+    if wl.dim != 2 or axis == "auto":
+        axis = "images" if (wl.dim == 2 and wl.n >= world) else "samples"
+    n_local, s_local = wl.n, wl.n_steps
+    if shard_on:
+        lo, hi = engine.Shard.range_of(rank, world, wl.n if axis == "images" else wl.n_steps)
+        if axis == "images":
+            n_local = hi - lo
+        else:
+            s_local = hi - lo
+    ex = build_explainer(wl, dev, args, dist_on=shard_on, n_local=n_local)
+    dt, records, out = timed(lambda: ex(xd, y), args.steps, args.warmup, world, dev)
+    assert out is not None
+    first = out[0] if isinstance(out, tuple) else out
+    assert np.isfinite(np.asarray(first)).all()
+    kern = kernel_table(records, args.steps)
+    units_per_step = n_local * s_local  # (item x sample) units this rank's launches processed
+    roof = roofline(wl, kern, args.steps, units_per_step, traffic)
+    if traffic and "error" in traffic:
+        roof["traffic_error"] = traffic["error"]
+
+    secondary = {}
+    if world > 1:
+        secondary["collectives"] = collectives_timing(wl, dev, world, axis)
+        exw = build_explainer(wl, dev, args, dist_on=False)  # each rank its own batch, no collective
+        dtw, _, _ = timed(lambda: exw(xd, y), 2, 1, world, dev)
+        secondary["weak_scaling"] = {"value": round(wl.n * 2 * world / dtw, 3), "ms_per_step": round(dtw / 2 * 1e3, 2),
+                                     "what": "each rank explains its own %d-item batch (no collective), 2 steps"
+                                             % wl.n}
+
+    cpu, cpu_ref = None, None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
-        cpu = cpu_baseline(args.cpu_seconds)
+        cpu, cpu_ref = cpu_baseline(wl, args.cpu_seconds, x, y)
+    extras = {}
+    if rank == 0 and world == 1 and wl.name == "c2" and args.extras == "auto":
+        extras = c2_extras(wl, dev, args, ex, xd, y, cpu_ref)
+    elif cpu_ref is not None and wl.name in ("c1",):
+        n_img, n_s, ref = cpu_ref
+        extras["parity"] = {"gpu_vs_cpu_reference": _cmp(out[:n_img], ref, "GPU vs CPU reference path, same input, "
+                                                                            "weights and numpy noise")}
 
-    total_attr = N_IMAGES * args.steps * world
+    model_dtype = args.model_dtype or wl.model_dtype
+    total = wl.n * args.steps
     if rank == 0:
         line = {
-            "metric": "WAM-2D attributions/sec @224^2 n_samples=25 (db4 J=3 SmoothGrad, ResNet-50)",
-            "value": round(total_attr / dt, 3), "unit": "attributions/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-            "data": "synthetic (RandomState(1) N(0,1) images, random-init ResNet-50)",
-            "config": {"workload": "c2: WAM-2D db4 J=3 SmoothGrad n_samples=25, batch 64 x 224x224, ResNet-50",
-                       "model_dtype": args.model_dtype, "global_batch": N_IMAGES * world, "seq_len": None,
-                       "parallelism": "dp%d" % world, "noise": "philox", "frame": "native(E1)",
-                       "sample_batch": args.sample_batch, "channels_last": args.channels_last,
-                       "model_exec": "autocast" if args.no_optimize_model else
-                       "optimize_model (BN folded into convs, polyphase stem input-gradient, bf16 weights)"},
-            "roofline": roofline, "cpu_baseline": cpu}
+            "metric": wl.metric, "value": round(total / dt, 3), "unit": wl.unit, "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2),
+            "higher_is_better": True, "scaling": "strong" if world > 1 else "weak", "vs_baseline": None,
+            "dtype": "fp32", "data": "synthetic inputs, random-init weights (no network)",
+            "config": {"workload": wl.describe, "model_dtype": model_dtype, "global_batch": wl.n,
+                       "seq_len": None, "parallelism": ("dp%d (%s axis)" % (world, axis))
+                       if world > 1 else "dp1",
+                       "sample_batch": getattr(ex, "sample_batch", None),
+                       "model_exec": "as is" if (args.no_optimize_model or wl.dim != 2 or wl.name == "c1") else
+                       "optimize_model (BN folded, polyphase stem input-gradient, fused epilogues)",
+                       "wam_arith": "fp32"},
+            "roofline": roof, "cpu_baseline": cpu}
+        line.update(secondary)
+        line.update(extras)
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
