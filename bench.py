@@ -56,6 +56,25 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0
+_T0 = time.time()
+
+
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    sys.stderr.write("[bench %6.1fs] %s\n" % (time.time() - _T0, msg))
+    sys.stderr.flush()
+
+
+def heartbeat(period=45.0):
+    """A daemon thread that reports every `period` s, so long phases (MIOpen searches, profiler
+    passes, the CPU baseline) are never mistaken for a hang."""
+    import threading
+
+    def run():
+        while True:
+            time.sleep(period)
+            log("alive")
+    threading.Thread(target=run, daemon=True).start()
 
 
 # ============================================================================ configurations
@@ -298,12 +317,14 @@ def _short_kernel(name):
 
 def _pmc_pass(counter, config, outdir):
     exe = shutil.which("rocprofv3")
+    log("rocprofv3 --pmc %s pass (child run of %s)" % (counter, config))
     cmd = ["timeout", "-s", "KILL", "150", exe, "--pmc", counter, "--kernel-include-regex", "k_[a-z0-9_]+",
            "--output-format", "csv", "-d", outdir, "-o", "run", "--", sys.executable, os.path.join(REPO, "bench.py"),
            "--config", config, "--wam-probe"]
     env = dict(os.environ, TMPDIR="/tmp")
     p = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=200)
     files = glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True)
+    log("rocprofv3 --pmc %s pass done (rc %d)" % (counter, p.returncode))
     if p.returncode != 0 or not files:
         raise RuntimeError("rocprofv3 --pmc %s failed (rc %d): %s" % (counter, p.returncode,
                                                                        p.stdout.decode(errors="replace")[-600:]))
@@ -475,6 +496,7 @@ def c2_extras(wl, dev, args, ex, x, y, cpu_ref):
         var = {}
         for tag, kw in (("fp32_model_folded", dict(model_dtype="fp32")),
                         ("bf16_autocast_model_as_is", dict(model_dtype="bf16", optimize=False))):
+            log("variant %s" % tag)
             e = build_explainer(wl, dev, args, **kw)
             dt, _, _ = timed(lambda: e(x, y), 2, 1, 1, dev)
             var[tag] = {"value": round(wl.n * 2 / dt, 3), "ms_per_step": round(dt / 2 * 1e3, 2), "steps": 2}
@@ -547,6 +569,7 @@ def main():
     args = parse()
     if args.wam_probe:
         return wam_probe(args)
+    heartbeat()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -579,6 +602,7 @@ def main():
         else:
             s_local = hi - lo
     ex = build_explainer(wl, dev, args, dist_on=shard_on, n_local=n_local)
+    log("%s: %d warm-up + %d timed steps on %d GPU(s)" % (wl.name, args.warmup, args.steps, world))
     dt, records, out = timed(lambda: ex(xd, y), args.steps, args.warmup, world, dev)
     assert out is not None
     first = out[0] if isinstance(out, tuple) else out
@@ -589,6 +613,7 @@ def main():
     if traffic and "error" in traffic:
         roof["traffic_error"] = traffic["error"]
 
+    log("timed: %.1f ms per step" % (dt / args.steps * 1e3))
     secondary = {}
     if world > 1:
         secondary["collectives"] = collectives_timing(wl, dev, world, axis)
@@ -600,9 +625,11 @@ def main():
 
     cpu, cpu_ref = None, None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+        log("cpu baseline (~%.0f s)" % args.cpu_seconds)
         cpu, cpu_ref = cpu_baseline(wl, args.cpu_seconds, x, y)
     extras = {}
     if rank == 0 and world == 1 and wl.name == "c2" and args.extras == "auto":
+        log("c2 extras: parity, variants, round trip, copy ceiling")
         extras = c2_extras(wl, dev, args, ex, xd, y, cpu_ref)
     elif cpu_ref is not None and wl.name in ("c1",):
         n_img, n_s, ref = cpu_ref

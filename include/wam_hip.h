@@ -229,6 +229,40 @@ int wam_disentangle_scales(const wam_plan* plan, int64_t items, const float* map
                            int approx, int size, double* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
+ * Wavelet-domain insertion / deletion / mu-fidelity (src/evaluation_helpers.py:
+ * 361-594 called by Eval2DWAM, src/evaluators.py:553-801). The reference's per-mask CPU loop
+ * pywt.wavedec2 -> coeffs_to_array -> arr * mask -> waverec2 -> uint8 -> ToTensor/Normalize
+ * becomes: wam_wavedec (mode symmetric) once per image, wam_coeff_masks, wam_waverec of all masks
+ * in one launch, wam_quantize_normalize.
+ * ---------------------------------------------------------------------------------------------- */
+/* generate_masks (:455-505) from a ranking: rank[p] = position of pixel p in the descending
+ * importance order; masks [n_iter + 1, len] float32: mask m = 1 where rank < thr(m), thr(0) = 0,
+ * thr(m) = m * n_comp, thr(n_iter) = len (deletion != 0: the complement). */
+int wam_rank_masks(int64_t n_iter, int64_t n_comp, int64_t len, const int32_t* rank, int deletion,
+                   float* masks, void* stream);
+/* arr * masks[m] in pywt.coeffs_to_array's layout: coefficient k (band-major item offset) of each
+ * of `items` planes sits at array position pos[k] (< mask_len). out: band-major coefficients of
+ * n_masks * items planes, plane (m, i) = m * items + i. */
+int wam_coeff_masks(const wam_plan* plan, int64_t items, const float* coeffs, const int32_t* pos,
+                    int64_t n_masks, int64_t mask_len, const float* masks, float* out, void* stream);
+/* per image (channels x plane floats): normalize_data (min-max, float32), (v * 255) -> uint8
+ * (truncation), / 255, (- mean[c]) / std[c] (torchvision ToTensor + Normalize); mean / std are
+ * HOST arrays of `channels` (<= 4) values. */
+int wam_quantize_normalize(int64_t images, int channels, int64_t plane, const float* rec, const float* mean,
+                           const float* std, float* out, void* stream);
+/* scipy.ndimage.gaussian_filter of items h x w float64 maps, mode 'reflect' (half-sample
+ * symmetric): weights[0..radius] = the symmetric 1-D kernel (host), axis 0 then axis 1, scipy's
+ * accumulation order; tmp: items * h * w doubles of scratch. */
+int wam_gaussian_filter2d(int64_t items, int h, int w, const double* weights, int radius, const double* in,
+                          double* tmp, double* out, void* stream);
+/* out[m, p] = grid[m, cell[p]]  (nearest-neighbour zoom through a precomputed cell map) */
+int wam_upsample_masks(int64_t n_masks, int64_t grid_len, const float* grid, int64_t out_len,
+                       const int32_t* cell, float* out, void* stream);
+/* sum_importance (:361-393): out[m] = sum_p wam[p] * grid[m, cell[p]] (float64) */
+int wam_masked_sums(int64_t n_masks, int64_t len, const double* wam, int64_t grid_len, const float* grid,
+                    const int32_t* cell, double* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
  * Explained-model input-gradient pass (lib/wam_2D.py:114-116: model forward, diag-mean loss,
  * backward). Not a ptwt replacement: fused elementwise steps of a BN-folded ReLU network, each one
  * HBM pass instead of the 2-4 torch kernels it replaces (wam_amd/model_fuse.py drives them).
