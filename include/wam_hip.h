@@ -262,6 +262,15 @@ int wam_upsample_masks(int64_t n_masks, int64_t grid_len, const float* grid, int
 int wam_masked_sums(int64_t n_masks, int64_t len, const double* wam, int64_t grid_len, const float* grid,
                     const int32_t* cell, double* out, void* stream);
 
+/* WaveletAttribution3D.visualize (lib/wam_3D.py:662-719): cube [items, S, S, S]
+ * float32 (the |grad| cube of smooth / IG) -> out [items, levels + 2, S, S, S] float32: per level
+ * the block (approximation corner, or add + ada + add + daa + dad + dda of the detail shell, as
+ * the reference sums them) upsampled by scipy.ndimage.zoom order 1 and divided by its max; slot
+ * levels + 1 = the level sum divided by its max over the batch. scratch: items * (levels + 1) + 1
+ * floats. WAM_ERR_SHAPE when S is not divisible as the reference's assignment needs. */
+int wam_visualize3d(int64_t items, int size, int levels, const float* cube, float* out, float* scratch,
+                    void* stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Explained-model input-gradient pass (lib/wam_2D.py:114-116: model forward, diag-mean loss,
  * backward). Not a ptwt replacement: fused elementwise steps of a BN-folded ReLU network, each one

@@ -311,3 +311,42 @@ def ig_3d(model, x, y=None, wavelet="haar", J=3, mode="symmetric", n_samples=25,
         path = [[c[0] * a] + [{k: v * a for k, v in d.items()} for d in c[1:]] for c in coeffs]
         gp[:, i] = single_pass_3d(model, path, y, wavelet, J, mode, inner_size or 16, shape=False)
     return base * np.trapz(np.nan_to_num(gp), axis=1)
+
+
+def visualize_3d(grads, J, input_size):
+    """WaveletAttribution3D.visualize (lib/wam_3D.py:662-719), incl. its orientation sum
+    (add + ada + add + daa + dad + dda) and the batch-wide max of the level sum."""
+    from scipy.ndimage import zoom
+    idx = [int(input_size / 2 ** j) for j in range(J + 1)][::-1]
+    idx.insert(0, 0)
+    vis = np.empty((grads.shape[0], J + 2) + grads.shape[1:], dtype=np.float32)
+    for i in range(grads.shape[0]):
+        for j in range(J + 1):
+            s, e = idx[j], idx[j + 1]
+            g = grads[i]
+            if s == 0:
+                c = g[:e, :e, :e]
+            else:
+                ada, add = g[:s, s:e, :s], g[:s, s:e, s:e]
+                daa, dad, dda = g[s:e, :s, :s], g[s:e, :s, s:e], g[s:e, s:e, :s]
+                c = add + ada + add + daa + dad + dda
+            up = zoom(c, int(input_size / c.shape[-1]), order=1)
+            vis[i, j] = up / up.max()
+    allv = np.sum(vis[:, :J + 1], axis=1)
+    vis[:, -1] = allv / allv.max()
+    return vis
+
+
+def filter_voxels_3d(grads, coeffs, EPS, wavelet):
+    """BaseWAM3D.filter_voxels (lib/wam_3D.py:439-495): approximation x min-max-normalised
+    gradient, details x (|g| / max(g) >= EPS), waverec3 per volume (float64 oracle)."""
+    from . import dwt
+    out = []
+    for grad, coeff in zip(grads, coeffs):
+        ag = (grad[0] - np.min(grad[0])) / (np.max(grad[0] - np.min(grad[0])))
+        rec = [coeff[0] * ag]
+        for dg_l, dc_l in zip(grad[1:], coeff[1:]):
+            rec.append({k: dc_l[k] * ((np.abs(dg_l[k]) / dg_l[k].max()) >= EPS) for k in dg_l})
+        out.append(dwt.waverec3([rec[0].astype(np.float64)] + [{k: v.astype(np.float64) for k, v in d.items()}
+                                                                 for d in rec[1:]], wavelet))
+    return np.array(out)

@@ -112,6 +112,15 @@ def test_disentangle_scales_oracle_vs_reference_goldens(name):
         assert not sc[:-1, kw["J"]].any() and sc[-1, kw["J"]].any()
 
 
+@pytest.mark.parametrize("name", ["vis_s32_j2", "vis_s16_j1", "vis_s64_j3"])
+def test_visualize_3d_oracle_vs_reference_goldens(name):
+    """Row f4: WaveletAttribution3D.visualize restated vs the reference's own outputs."""
+    from tests.golden.make_f4_goldens import VIS_CASES, cube
+    n, S, J, seed = VIS_CASES[name]
+    got = wam_ref.visualize_3d(cube(n, S, seed), J, S)
+    assert np.array_equal(got, npz("f4_goldens.npz")[name])
+
+
 def test_level_sizes_match_survey():
     """SURVEY.md section 8 coefficient sizes per config (pywt-verified there)."""
     L = lambda w: len(dwt.filter_bank(w)[0])

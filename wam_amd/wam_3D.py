@@ -6,7 +6,11 @@ same constructor arguments, call signatures, float32 cube outputs and side attri
 steps) are transformed in one launch instead of the reference's per-volume Python loop
 (:193); the |grad| cube packing (``refactor``) is a gather map over the band-major gradients;
 the reference's in-loop averaging of ``smooth`` (:585-587, result = sum_s cube_s * n^-(n-s)) is
-reproduced exactly. Point clouds are not implemented in the reference either (:381-383).
+reproduced exactly. Point clouds are not implemented in the reference either (:381-383): the entry
+prints 'Not implemented yet' as there; its unreachable ``evaluate_point_clouds`` (:247-358) is
+provided on the GPU 1D kernels. Post-processing: ``visualize`` (:662-719) is
+the k_vis3d_* kernels; ``filter_voxels`` (:439-495) thresholds on the device and reconstructs with
+the 3D synthesis kernels.
 Build-only kwargs: noise, frame ('legacy' keeps the inner 16^3 refactor size of IG), sample_batch,
 autocast_dtype, dist.
 """
@@ -17,6 +21,7 @@ from . import frames
 from .constants import KEYS3
 from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, legacy3d_weights, legacy_noise,
                      model_device, require_gpu_device)
+from ._lib import check, lib, ptr, stream_of
 from .plan import cube_accumulate, get_plan, item_sigma, noise_add, subband_maps
 
 
@@ -42,6 +47,8 @@ class BaseWAM3D:
         self.autocast_dtype = autocast_dtype
         self._coeffs_src = None
         self._coeffs = None
+        self._grads_src = None
+        self._grads = None
 
     @property
     def _dev(self):
@@ -64,6 +71,89 @@ class BaseWAM3D:
     @coeffs.setter
     def coeffs(self, v):
         self._coeffs = v
+
+    @staticmethod
+    def _item_lists(plan, flat, items, first, n, c):
+        views = [v[first * c:(first + n) * c].detach().cpu().numpy() for v in plan.split(flat, items)]
+        out = []
+        for k in range(n):
+            sq = [views[b][k * c:(k + 1) * c].squeeze() for b in range(plan.nbands)]
+            out.append([sq[0]] + [{key: sq[1 + 7 * lv + j] for j, key in enumerate(KEYS3)}
+                                  for lv in range(plan.levels)])
+        return out
+
+    @property
+    def grads(self):
+        """Per-volume coefficient gradients of the last evaluate_voxels pass (the reference's
+        detached_grads, lib/wam_3D.py:241; filter_voxels reads them); WaveletAttribution3D
+        overwrites it with the |grad| cube, as the reference does (:589)."""
+        if self._grads is None and self._grads_src is not None:
+            self._grads = self._item_lists(*self._grads_src)
+        return self._grads
+
+    @grads.setter
+    def grads(self, v):
+        self._grads = v
+        self._grads_src = None
+
+    def filter_voxels(self, normalized=True):
+        """lib/wam_3D.py:439-495: keep the coefficients whose normalised gradient passes EPS and
+        reconstruct: approximation x min-max-normalised gradient; details x (|g| / max(g) >= EPS)
+        (max of the SIGNED gradient, as the reference). Masks on the device, waverec3 on the 3D
+        synthesis kernels; returns [N, D, H, W] float32 (one reconstruction per volume; the
+        reference hands ptwt.waverec3 squeezed 3-D coefficients)."""
+        grads, coeffs = self.grads, self.coeffs
+        if grads is None or coeffs is None:
+            raise AttributeError("filter_voxels needs the coefficient gradients and coefficients of a pass")
+        out = []
+        dev = self._dev
+        for grad, coeff in zip(grads, coeffs):
+            if not isinstance(grad, (list, tuple)):
+                raise AttributeError("'numpy.ndarray' object has no attribute 'keys'")  # the |grad| cube
+            g0 = torch.as_tensor(np.asarray(grad[0]), dtype=torch.float32, device=dev)
+            ag = (g0 - g0.min()) / (g0 - g0.min()).max()
+            bands = [torch.as_tensor(np.asarray(coeff[0]), dtype=torch.float32, device=dev) * ag]
+            for dg_l, dc_l in zip(grad[1:], coeff[1:]):
+                for key in KEYS3:
+                    dg = torch.as_tensor(np.asarray(dg_l[key]), dtype=torch.float32, device=dev)
+                    dc = torch.as_tensor(np.asarray(dc_l[key]), dtype=torch.float32, device=dev)
+                    bands.append(dc * ((dg.abs() / dg.max()) >= self.EPS).float())
+            from .filters import get_wavelet
+            L = len(get_wavelet(self.wavelet).dec_lo)
+            fin = bands[-1].shape
+            plan = get_plan(3, tuple(2 * m + 2 - L if L > 2 else 2 * m for m in fin), len(grad) - 1, self.wavelet,
+                            self.mode, dev)
+            flat = torch.cat([b.reshape(-1) for b in bands])
+            out.append(plan.waverec(flat, 1)[0][0].cpu().numpy())
+        return np.array(out)
+
+    def evaluate_point_clouds(self, x, y, permute):
+        """lib/wam_3D.py:247-358 (unreachable from __call__ in the reference, which prints 'Not
+        implemented yet'): 1D wavedec of the flattened [B, N*3] coordinates, waverec, the model on
+        the [B, N, 3] reconstruction (a tuple-returning point net when permute is given), the
+        diag-mean loss, coefficient gradients by the adjoint. Returns (coeffs, coeffs) as the
+        reference does (:358); the gradients are kept in self.point_grads."""
+        dev = self._dev
+        x = torch.as_tensor(x).detach().to(dev, torch.float32).contiguous()
+        self.batch_size, self.shape_size = x.shape[0], x.shape[1]
+        self.input = x.cpu().numpy()
+        flat_x = x.view(x.shape[0], -1)
+        plan = get_plan(1, (flat_x.shape[1],), self.J, self.wavelet, "reflect", dev)  # ptwt.wavedec's default mode
+        z = plan.wavedec(flat_x)
+        rec = plan.waverec(z, x.shape[0])[0][:, :flat_x.shape[1]].reshape(x.shape)
+        leaf = rec.detach().requires_grad_(True)
+        with torch.enable_grad():
+            out = self.model(leaf.permute(permute)) if permute is not None else self.model(leaf)
+            if isinstance(out, tuple):
+                out = out[0]
+            loss = torch.diag(out[:, y]).mean()
+            (g,) = torch.autograd.grad(loss, leaf)
+        g_full = torch.zeros((x.shape[0],) + plan.rec_shape, device=dev)
+        g_full[:, :flat_x.shape[1]] = g.reshape(x.shape[0], -1)
+        cg = plan.adjoint(g_full)
+        coeffs = [v.cpu().numpy() for v in plan.split(z, x.shape[0])]
+        self.point_grads = [v.cpu().numpy() for v in plan.split(cg, x.shape[0])]
+        return coeffs, coeffs
 
     def refactor(self, coeffs, input_size=16):
         """lib/wam_3D.py:127-166 on host coefficient lists (API compatibility)."""
@@ -140,6 +230,8 @@ class BaseWAM3D:
         cg = self._grads(plan, flat, n * c, y, 1, n, c)
         self._coeffs_src = (plan, flat, n * c, 0, n, c)
         self._coeffs = None
+        self._grads_src = (plan, cg, n * c, 0, n, c)
+        self._grads = None
         S = self.input_size if self.input_size is not None else 16
         if self.input_size is None:
             self.input_size = S
@@ -219,9 +311,24 @@ class WaveletAttribution3D(BaseWAM3D):
             self.wam._coeffs_src = (plan, flat, cnt * n * c, (cnt - 1) * n, n, c)
             self.wam._coeffs = None
         shard.all_reduce_sum(acc)
-        out = acc.view(n, S, S, S).cpu().numpy()
+        self._cube_dev = acc.view(n, S, S, S)
+        out = self._cube_dev.cpu().numpy()
         self.grads = out
         return out
+
+    def visualize(self):
+        """lib/wam_3D.py:662-719 on the device: [N, J + 2, S, S, S] float32 -- per level the
+        (approximation / six-orientation sum) block upsampled by scipy zoom order 1 and divided by
+        its max, then the level sum divided by its batch max (wam_visualize3d)."""
+        dev = self._dev
+        cube = getattr(self, "_cube_dev", None)
+        if cube is None or not isinstance(self.grads, np.ndarray) or cube.shape != self.grads.shape:
+            cube = torch.as_tensor(np.ascontiguousarray(self.grads, dtype=np.float32)).to(dev)
+        n, S = cube.shape[0], cube.shape[-1]
+        out = torch.empty((n, self.J + 2, S, S, S), dtype=torch.float32, device=dev)
+        scratch = torch.empty(n * (self.J + 1) + 1, dtype=torch.float32, device=dev)
+        check(lib.wam_visualize3d(n, S, self.J, ptr(cube.contiguous()), ptr(out), ptr(scratch), stream_of(dev)))
+        return out.cpu().numpy()
 
     def alter(self, alpha, coeffs):
         """lib/wam_3D.py:594-611."""
@@ -276,7 +383,8 @@ class WaveletAttribution3D(BaseWAM3D):
                 wk = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
                 self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 1, weights=wk)
         shard.all_reduce_sum(acc)
-        out = (base.view(n, S, S, S) * acc.view(n, S, S, S)).cpu().numpy()
+        self._cube_dev = base.view(n, S, S, S) * acc.view(n, S, S, S)
+        out = self._cube_dev.cpu().numpy()
         self.grads = out
         return out
 
