@@ -509,20 +509,24 @@ def c2_extras(wl, dev, args, ex, x, y, cpu_ref):
     r = p.waverec(p.wavedec(xd), xd.shape[0])[0][:, :224, :224]
     extras["roundtrip"] = {"max_abs": float((r - xd).abs().max()), "max_abs_input": float(xd.abs().max()),
                            "what": "db4 J=3 reflect wavedec2 -> waverec2 of the 64x3 input planes (fp32)"}
-    # copy ceiling: device-to-device copy of 2 GiB
+    # copy ceiling: libwam_hip.so's streaming copy (16-B loads / stores) and torch's, 2 GiB each
+    from wam_amd._lib import check as _check, lib as _lib, ptr as _ptr, stream_of as _stream_of
     a = torch.empty(512 << 20, dtype=torch.float32, device=dev)
     bb = torch.empty_like(a)
-    bb.copy_(a)
-    torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        bb.copy_(a)
-    e1.record()
-    torch.cuda.synchronize(dev)
-    ms = e0.elapsed_time(e1) / 10
-    extras["copy_ceiling"] = {"GBps": round(2 * a.numel() * 4 / (ms * 1e-3) / 1e9, 1), "bytes": 2 * a.numel() * 4,
-                              "what": "torch device copy of 2 GiB (read + write), mean of 10"}
+    nbytes = a.numel() * 4
+    ceil = {}
+    for tag, fn in (("k_copy", lambda: _check(_lib.wam_copy(nbytes, _ptr(a), _ptr(bb), _stream_of(dev)))),
+                    ("torch_copy", lambda: bb.copy_(a))):
+        fn()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            fn()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        ceil[tag + "_GBps"] = round(2 * nbytes / (e0.elapsed_time(e1) / 10 * 1e-3) / 1e9, 1)
+    extras["copy_ceiling"] = dict(ceil, bytes=2 * nbytes, what="2 GiB device copy (read + write), mean of 10")
     del a, bb
     return extras
 

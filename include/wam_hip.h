@@ -135,6 +135,8 @@ int wam_waverec_adjoint_maps(const wam_plan* plan, int64_t groups, int64_t group
  * (names: 64 chars each) and clears the log. Returns the number of records copied.
  * ---------------------------------------------------------------------------------------------- */
 int wam_timing_enable(int on);
+/* dst = src (bytes % 16 == 0, 16-B aligned): a streaming copy kernel, the measured HBM ceiling */
+int wam_copy(int64_t bytes, const void* src, void* dst, void* stream);
 int wam_timing_drain(int max_records, char* names, float* ms, double* bytes);
 
 /* ------------------------------------------------------------------------------------------------

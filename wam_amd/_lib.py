@@ -62,6 +62,7 @@ _SIGS = {
                                      c_vp]),
     "wam_waverec_adjoint_maps": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "wam_timing_enable": (c_int, [c_int]),
+    "wam_copy": (c_int, [c_i64, c_vp, c_vp, c_vp]),
     "wam_visualize3d": (c_int, [c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "wam_rank_masks": (c_int, [c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp]),
     "wam_coeff_masks": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),

@@ -438,6 +438,14 @@ __global__ void __launch_bounds__(256) k_disentangle(int64_t items, int size, in
   }
 }
 
+
+// Streaming copy (16-B loads / stores, grid-stride): the measured HBM ceiling bench.py reports
+// beside the 8 TB/s spec peak.
+__global__ void __launch_bounds__(256) k_copy(int64_t n4, const float4* __restrict__ src, float4* __restrict__ dst) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n4; t += (int64_t)gridDim.x * blockDim.x)
+    dst[t] = src[t];
+}
+
 }  // namespace
 
 extern "C" {
@@ -609,6 +617,18 @@ int wam_disentangle_scales(const wam_plan* plan, int64_t items, const float* map
   WamTimer tm((hipStream_t)stream, "k_disentangle", 4.0 * items * g.item + 8.0 * work);
   hipLaunchKernelGGL(k_disentangle, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, items, size, approx,
                      g, maps, band_max, out);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int wam_copy(int64_t bytes, const void* src, void* dst, void* stream) {
+  if (bytes < 0 || (bytes & 15) || !src || !dst || ((uintptr_t)src & 15) || ((uintptr_t)dst & 15))
+    return WAM_ERR_INVALID_ARG;
+  const int64_t n4 = bytes / 16;
+  if (n4 == 0) return WAM_OK;
+  WamTimer tm((hipStream_t)stream, "k_copy", 2.0 * bytes);
+  hipLaunchKernelGGL(k_copy, dim3(wam_grid(n4, 256, 256 * 64)), dim3(256), 0, (hipStream_t)stream, n4,
+                     (const float4*)src, (float4*)dst);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }

@@ -48,7 +48,7 @@ class BaseWAM3D:
         self._coeffs_src = None
         self._coeffs = None
         self._grads_src = None
-        self._grads = None
+        self._grad_lists = None
 
     @property
     def _dev(self):
@@ -87,13 +87,13 @@ class BaseWAM3D:
         """Per-volume coefficient gradients of the last evaluate_voxels pass (the reference's
         detached_grads, lib/wam_3D.py:241; filter_voxels reads them); WaveletAttribution3D
         overwrites it with the |grad| cube, as the reference does (:589)."""
-        if self._grads is None and self._grads_src is not None:
-            self._grads = self._item_lists(*self._grads_src)
-        return self._grads
+        if self._grad_lists is None and self._grads_src is not None:
+            self._grad_lists = self._item_lists(*self._grads_src)
+        return self._grad_lists
 
     @grads.setter
     def grads(self, v):
-        self._grads = v
+        self._grad_lists = v
         self._grads_src = None
 
     def filter_voxels(self, normalized=True):
@@ -231,7 +231,7 @@ class BaseWAM3D:
         self._coeffs_src = (plan, flat, n * c, 0, n, c)
         self._coeffs = None
         self._grads_src = (plan, cg, n * c, 0, n, c)
-        self._grads = None
+        self._grad_lists = None
         S = self.input_size if self.input_size is not None else 16
         if self.input_size is None:
             self.input_size = S
