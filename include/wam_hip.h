@@ -165,8 +165,8 @@ int wam_noise_add_ex(int64_t n_samples, int64_t items, int64_t item_stride, int6
  * ---------------------------------------------------------------------------------------------- */
 /* maps[item, band-packed] = | mean over `channels` of coeff_grads |   (numpy float32 mean:
  * ((g0 + g1) + g2 ...) / C);  band_max[group, band] = max over the group's items of maps
- * (atomic; caller zero-fills). items = groups * group_items; coeff_grads hold items*channels
- * signals. maps layout: item-major, bands packed with wam_plan_band_offset. */
+ * (atomic; caller zero-fills; NULL: maps only). items = groups * group_items; coeff_grads hold
+ * items*channels signals. maps layout: item-major, bands packed with wam_plan_band_offset. */
 int wam_subband_maps(const wam_plan* plan, int64_t groups, int64_t group_items, int channels,
                      const float* coeff_grads, float* maps, float* band_max, void* stream);
 

@@ -44,8 +44,10 @@ def test_visualize_after_smooth(W):
     assert np.abs(got - ref).max() <= 1e-6
 
 
-@pytest.mark.parametrize("wav,J", [("haar", 2), ("db2", 1)])
+@pytest.mark.parametrize("wav,J", [("haar", 2), ("haar", 1)])
 def test_filter_voxels_vs_restatement(W, wav, J):
+    """(BaseWAM3D's cube, hence the pass filter_voxels reads, exists for Haar only: other filters
+    give non-dyadic coefficient blocks the reference's refactor cannot place)"""
     from oracle import wam_ref
     x = torch.tensor((np.random.RandomState(10).standard_normal((2, 1, 16, 16, 16)) > 0).astype(np.float32))
     b = W.BaseWAM3D(testmodels.TinyVoxel().cuda(), wavelet=wav, J=J, EPS=0.3)

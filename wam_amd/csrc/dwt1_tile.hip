@@ -14,15 +14,31 @@
 // percent. Boundary modes: zero, reflect, symmetric, constant (periodic extensions are not local
 // and stay on the per-axis kernels).
 #include <algorithm>
+#include <mutex>
+#include <set>
 
 #include "kernels.hpp"
 
 namespace {
 
+// opt in to more than 64 KB of dynamic LDS, once per (kernel, device)
+int lds_opt_in(const void* kern, int bytes) {
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> done;
+  if (bytes <= 64 * 1024) return WAM_OK;
+  int dev = 0;
+  WAM_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  if (done.count({kern, dev})) return WAM_OK;
+  WAM_HIP_CHECK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  done.insert({kern, dev});
+  return WAM_OK;
+}
+
 constexpr int kT1 = 512;          // threads per workgroup (analysis)
 constexpr int kT1S = 256;         // threads per workgroup (synthesis)
-constexpr int kTile0 = 2048;      // finest-level outputs per tile (source window ~2 x this)
-constexpr int kLds1Cap = 64 * 1024;
+constexpr int kTile0 = 4096;      // finest-level outputs per tile (source window ~2 x this)
+constexpr int kLds1Cap = 80 * 1024;  // two workgroups per CU
 
 struct Dwt1Geom {
   int J;
@@ -87,14 +103,17 @@ __host__ __device__ __forceinline__ void ana_ranges(const Dwt1Geom& g, int tile,
   }
 }
 
+// tiles [t_lo, t_hi) are left to k_dwt1_ana_int; this kernel runs the others (nb per signal)
 template <int L>
 __global__ void __launch_bounds__(kT1) k_dwt1_ana(const float* __restrict__ in, float* __restrict__ coeffs,
-                                                 const float* __restrict__ filt, Dwt1Geom g) {
+                                                 const float* __restrict__ filt, Dwt1Geom g, int t_lo, int t_hi) {
   constexpr int p = L - 2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
-  const int64_t item = blockIdx.x / g.tiles;
-  const int tile = (int)(blockIdx.x % g.tiles);
+  const int nb = g.tiles - (t_hi - t_lo);
+  const int64_t item = blockIdx.x / nb;
+  const int kb = (int)(blockIdx.x % nb);
+  const int tile = kb < t_lo ? kb : t_hi + (kb - t_lo);
   float flo[L], fhi[L];
 #pragma unroll
   for (int k = 0; k < L; ++k) {
@@ -177,6 +196,113 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana(const float* __restrict__ in, 
       if (!last) smem[out_off + i - Sl] = a;
     }
     __syncthreads();
+  }
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// Interior tiles (no boundary extension at any level): persistent workgroups over (signal, tile)
+// units. Ranges are closed-form: coarsest computed range [S, E) = [t tj, (t + 1) tj), finer levels
+// S_l = 2 S_(l+1) - p, E_l = 2 E_(l+1). The source window and every approximation level live in
+// LDS de-interleaved (even / odd samples in separate arrays, the odd array offset by 16 banks), so
+// output r reads E[r + m], O[r + m]: consecutive lanes hit consecutive banks and the taps keep the
+// k = 0..L-1 fma order of the per-axis kernels (same sums). The next unit's window is fetched into
+// registers before the current unit's levels run, hiding its HBM latency.
+constexpr int kPF = 20;          // window floats prefetched per thread (window <= kPF * kT1)
+
+__host__ __device__ __forceinline__ int eo_cap(int n) { return (((n + 1) / 2 + 31) & ~31) + 16; }
+
+template <int L>
+__global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ in, float* __restrict__ coeffs,
+                                                     const float* __restrict__ filt, Dwt1Geom g, int t_lo, int t_hi,
+                                                     int64_t units) {
+  constexpr int p = L - 2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  float flo[L], fhi[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    flo[k] = filt[k];
+    fhi[k] = filt[L + k];
+  }
+  const int J = g.J;
+  const int nti = t_hi - t_lo;
+  const int tj = g.tile_j;
+  const int n0 = (tj << (J - 1)) + p * ((1 << (J - 1)) - 1);  // level-0 computed outputs per tile
+  const int wlen = 2 * n0 + p;
+  const int cw = eo_cap(wlen);            // window: E at [0, cw), O at [cw, 2 cw)
+  const int c0 = eo_cap(n0);              // level buffers (ping-pong): A at 2 cw, B after it
+  float* winE = smem;
+  float* winO = smem + cw;
+  const int c1 = eo_cap((n0 - p) >> 1);
+  float* bufA = smem + 2 * cw;            // even levels' outputs (level 0: n0 values)
+  float* bufB = bufA + 2 * c0;            // odd levels' outputs (level 1: (n0 - p) / 2 values)
+  auto unit_geom = [&](int64_t u, int64_t& item, int& tile, int& S0) {
+    item = u / nti;
+    tile = t_lo + (int)(u - item * nti);
+    S0 = ((tile * tj) << (J - 1)) - p * ((1 << (J - 1)) - 1);
+  };
+  float pf[kPF];
+  auto prefetch = [&](int64_t u) {
+    int64_t item;
+    int tile, S0;
+    unit_geom(u < units ? u : units - 1, item, tile, S0);
+    const float* x = in + item * (int64_t)g.n + (2 * S0 - p);
+#pragma unroll
+    for (int r = 0; r < kPF; ++r) {
+      const int j = tid + r * kT1;
+      pf[r] = x[j < wlen ? j : wlen - 1];
+    }
+  };
+  int64_t u = blockIdx.x;
+  if (u < units) prefetch(u);
+  for (; u < units; u += gridDim.x) {
+    int64_t item;
+    int tile, S0;
+    unit_geom(u, item, tile, S0);
+#pragma unroll
+    for (int r = 0; r < kPF; ++r) {
+      const int j = tid + r * kT1;
+      if (j < wlen) ((j & 1) ? winO : winE)[j >> 1] = pf[r];
+    }
+    __syncthreads();
+    prefetch(u + gridDim.x);  // in flight while the levels run
+    // level l: inputs (E, O) of length nin, outputs r in [0, nl), absolute index S_l + r
+    const float* iE = winE;
+    const float* iO = winO;
+    int Sl = S0, nl = n0;
+    for (int l = 0; l < J; ++l) {
+      const bool last = l == J - 1;
+      float* oE = (l & 1) ? bufB : bufA;
+      float* oO = oE + ((l & 1) ? c1 : c0);
+      const int ml = g.m[l];
+      const int T = tj << (J - 1 - l);                       // own outputs per tile at this level
+      const int own0 = tile * T;
+      float* dout = coeffs + g.items * g.off_d[l] + item * (int64_t)ml;
+      float* aout = coeffs + g.items * g.off_a + item * (int64_t)ml;
+      for (int r = tid; r < nl; r += kT1) {
+        float a = 0.f, d = 0.f;
+#pragma unroll
+        for (int m2 = 0; m2 < L / 2; ++m2) {
+          const float ve = iE[r + m2], vo = iO[r + m2];
+          a = fmaf(flo[2 * m2], ve, a);
+          d = fmaf(fhi[2 * m2], ve, d);
+          a = fmaf(flo[2 * m2 + 1], vo, a);
+          d = fmaf(fhi[2 * m2 + 1], vo, d);
+        }
+        const int i = Sl + r;
+        if (i >= own0 && i < own0 + T) {
+          dout[i] = d;
+          if (last) aout[i] = a;
+        }
+        if (!last) ((r & 1) ? oO : oE)[r >> 1] = a;
+      }
+      __syncthreads();
+      iE = oE;
+      iO = oO;
+      Sl = (Sl + p) >> 1;
+      nl = (nl - p) >> 1;
+    }
   }
 }
 
@@ -299,6 +425,37 @@ int ana_lds_bytes(const wam_plan* p, const Dwt1Geom& g) {
   return best * 4;
 }
 
+// interior tiles: every level's computed range and taps inside the signal, own range complete
+bool tile_interior(const Dwt1Geom& g, int tile, int p) {
+  int S = tile * g.tile_j, E = (tile + 1) * g.tile_j;
+  for (int l = g.J - 1; l >= 0; --l) {
+    const int T = g.tile_j << (g.J - 1 - l);
+    const int nin = l ? g.m[l - 1] : g.n;
+    if (S < 0 || E > g.m[l] || (tile + 1) * T > g.m[l]) return false;
+    if (2 * S - p < 0 || 2 * E - 1 >= nin) return false;
+    if (l) {
+      S = 2 * S - p;
+      E = 2 * E;
+    }
+  }
+  return true;
+}
+
+void interior_range(const Dwt1Geom& g, int p, int& t_lo, int& t_hi) {
+  t_lo = t_hi = 0;
+  int t = 0;
+  while (t < g.tiles && !tile_interior(g, t, p)) ++t;
+  t_lo = t;
+  while (t < g.tiles && tile_interior(g, t, p)) ++t;
+  t_hi = t;
+  if (t_hi <= t_lo) t_lo = t_hi = 0;
+}
+
+int ana_int_lds_bytes(const Dwt1Geom& g, int p) {
+  const int n0 = (g.tile_j << (g.J - 1)) + p * ((1 << (g.J - 1)) - 1);
+  return (2 * eo_cap(2 * n0 + p) + 2 * eo_cap(n0) + 2 * eo_cap((n0 - p) >> 1)) * 4;
+}
+
 int syn_lds_bytes(const wam_plan* p) {
   // level-0 coefficient range of a 2*kTile0 output tile: kTile0 + L/2 (+ the H2 zero pads)
   const int cap = ((kTile0 + 2 * p->L + 8) + 63) & ~63;
@@ -325,18 +482,53 @@ int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in,
   const int64_t blocks = batch * g.tiles;
   if (blocks > 0x7fffffff) return WAM_ERR_UNSUPPORTED;
   const int lds = ana_lds_bytes(p, g);
-  WamTimer tm(st, "k_dwt1_ana", 4.0 * (double)batch * ((double)n + (double)p->band_off[p->nbands]));
-  switch (p->L) {
+  const int pp = p->L - 2;
+  int t_lo, t_hi;
+  interior_range(g, pp, t_lo, t_hi);
+  const int n0 = (g.tile_j << (g.J - 1)) + pp * ((1 << (g.J - 1)) - 1);
+  const int lds_i = ana_int_lds_bytes(g, pp);
+  if (2 * n0 + pp > kPF * kT1 || lds_i > kLds1Cap) t_lo = t_hi = 0;  // window too long: all tiles generic
+  const int64_t units = batch * (int64_t)(t_hi - t_lo);
+  const int64_t nb_blocks = batch * (int64_t)(g.tiles - (t_hi - t_lo));
+  const double bytes = 4.0 * (double)batch * ((double)n + (double)p->band_off[p->nbands]);
+  if (units > 0) {
+    // persistent grid: two 512-thread workgroups per CU (LDS ~60 KB each)
+    int dev = 0;
+    WAM_HIP_CHECK(hipGetDevice(&dev));
+    int cus = 256;
+    WAM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int64_t grid = std::min<int64_t>(units, 2LL * cus);
+    WamTimer tm(st, "k_dwt1_ana_int", bytes * (double)(t_hi - t_lo) / g.tiles);
+    switch (p->L) {
+#define WAM_D1AI(LL)                                                                                            \
+  case LL:                                                                                                      \
+    if (int rc = lds_opt_in((const void*)k_dwt1_ana_int<LL>, lds_i)) return rc;                                \
+    hipLaunchKernelGGL(k_dwt1_ana_int<LL>, dim3((unsigned)grid), dim3(kT1), lds_i, st, in, coeffs, filt, g, t_lo, \
+                       t_hi, units);                                                                            \
+    break;
+      WAM_D1AI(2) WAM_D1AI(4) WAM_D1AI(6) WAM_D1AI(8) WAM_D1AI(10) WAM_D1AI(12) WAM_D1AI(14) WAM_D1AI(16)
+      WAM_D1AI(18) WAM_D1AI(20)
+#undef WAM_D1AI
+      default: return WAM_ERR_UNSUPPORTED;
+    }
+    WAM_LAUNCH_CHECK();
+  }
+  if (nb_blocks > 0) {
+    WamTimer tm(st, "k_dwt1_ana", bytes * (double)(g.tiles - (t_hi - t_lo)) / g.tiles);
+    switch (p->L) {
 #define WAM_D1A(LL)                                                                                          \
   case LL:                                                                                                   \
-    hipLaunchKernelGGL(k_dwt1_ana<LL>, dim3((unsigned)blocks), dim3(kT1), lds, st, in, coeffs, filt, g); \
+    if (int rc = lds_opt_in((const void*)k_dwt1_ana<LL>, lds)) return rc;                                    \
+    hipLaunchKernelGGL(k_dwt1_ana<LL>, dim3((unsigned)nb_blocks), dim3(kT1), lds, st, in, coeffs, filt, g, t_lo, \
+                       t_hi);                                                                                \
     break;
-    WAM_D1A(2) WAM_D1A(4) WAM_D1A(6) WAM_D1A(8) WAM_D1A(10) WAM_D1A(12) WAM_D1A(14) WAM_D1A(16) WAM_D1A(18)
-    WAM_D1A(20)
+      WAM_D1A(2) WAM_D1A(4) WAM_D1A(6) WAM_D1A(8) WAM_D1A(10) WAM_D1A(12) WAM_D1A(14) WAM_D1A(16) WAM_D1A(18)
+      WAM_D1A(20)
 #undef WAM_D1A
-    default: return WAM_ERR_UNSUPPORTED;
+      default: return WAM_ERR_UNSUPPORTED;
+    }
+    WAM_LAUNCH_CHECK();
   }
-  WAM_LAUNCH_CHECK();
   return WAM_OK;
 }
 
@@ -358,6 +550,7 @@ int launch_dwt1_tile_synthesis(const wam_plan* p, int64_t batch, const float* co
     switch (p->L) {
 #define WAM_D1S(LL)                                                                                            \
   case LL:                                                                                                     \
+    if (int rc = lds_opt_in((const void*)k_dwt1_syn<LL>, lds)) return rc;                                      \
     hipLaunchKernelGGL(k_dwt1_syn<LL>, dim3((unsigned)blocks), dim3(kT1S), lds, st, coeffs, o, filt, g, nout, sc); \
     break;
       WAM_D1S(2) WAM_D1S(4) WAM_D1S(6) WAM_D1S(8) WAM_D1S(10) WAM_D1S(12) WAM_D1S(14) WAM_D1S(16) WAM_D1S(18)

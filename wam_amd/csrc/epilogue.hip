@@ -125,7 +125,7 @@ struct BandTable {
   int32_t tile0[WAM_MAX_BANDS + 1];  // first tile of each band (prefix over ceil(nb / TILE))
   int nbands;
 };
-constexpr int kMapTile = 1024;  // elements per block (4 per thread)
+constexpr int kMapTile = 8192;  // elements per block (32 per thread): one band-max atomic per 32 KB
 
 // grid: x = tile (over all bands), y = item. One atomic max per block.
 __global__ void __launch_bounds__(256) k_subband_maps(BandTable bt, int64_t items_total, int64_t group_items,
@@ -157,7 +157,7 @@ __global__ void __launch_bounds__(256) k_subband_maps(BandTable bt, int64_t item
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (lane == 0) sm[wv] = m;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && band_max) {  // band_max == NULL: maps only (3D cube, no normalisation)
     for (int w = 1; w < 4; ++w) m = nan_max(m, sm[w]);
     const int64_t grp = item / group_items;
     // non-negative floats order like their bit patterns; NaN (0x7fc00000) wins like numpy's max
@@ -498,8 +498,7 @@ int wam_noise_add(int64_t n_samples, int64_t items, int64_t item_stride, int64_t
 
 int wam_subband_maps(const wam_plan* p, int64_t groups, int64_t group_items, int channels, const float* coeff_grads,
                      float* maps, float* band_max, void* stream) {
-  if (!p || groups < 0 || group_items < 0 || channels < 1 || !coeff_grads || !maps || !band_max)
-    return WAM_ERR_INVALID_ARG;
+  if (!p || groups < 0 || group_items < 0 || channels < 1 || !coeff_grads || !maps) return WAM_ERR_INVALID_ARG;
   int64_t items = groups * group_items;
   if (items == 0) return WAM_OK;
   if (items > 65535) return WAM_ERR_UNSUPPORTED;

@@ -215,12 +215,15 @@ def noise_add(x, sigma, n_samples, items, item_stride, noised_len, seed=0, sampl
     return out
 
 
-def subband_maps(plan, coeff_grads, groups, group_items, channels, maps=None, band_max=None):
+def subband_maps(plan, coeff_grads, groups, group_items, channels, maps=None, band_max=None, want_max=True):
+    """|channel mean| maps (item-major) and per-group band maxima (None when want_max=False)."""
     items = groups * group_items
     dev = coeff_grads.device
     if maps is None:
         maps = torch.empty(items * plan.coeff_numel, dtype=torch.float32, device=dev)
-    if band_max is None:
+    if not want_max:
+        band_max = None
+    elif band_max is None:
         band_max = torch.zeros((groups, plan.nbands), dtype=torch.float32, device=dev)
     else:
         band_max.zero_()

@@ -196,7 +196,7 @@ class BaseWAM3D:
 
     def _cube_from_grads(self, plan, cg, items, groups, n, input_size, acc, mode, n_total=1.0, weights=None,
                          prev=None, k0=0):
-        maps, _ = subband_maps(plan, cg, groups, n, 1)
+        maps, _ = subband_maps(plan, cg, groups, n, 1, want_max=False)  # the cube is not normalised
         src = frames.cube_map(plan, input_size, cg.device)
         cube_accumulate(groups, k0, n, src, maps, plan.coeff_numel, mode, n_total, acc, prev=prev, weights=weights)
 
