@@ -42,3 +42,11 @@ def melspec_db(wave, n_fft, sample_rate, n_mels):
     mel = torch.matmul(power.transpose(-1, -2), fb)   # [B, frames, n_mels]
     db = 10.0 * torch.log10(torch.clamp(mel, min=1e-10))
     return db.unsqueeze(1)
+
+
+def melspec_power(wave, n_fft, sample_rate, n_mels):
+    """torchaudio MelSpectrogram (power, no dB) of [B, T] -> [B, n_mels, frames]."""
+    fb, win = mel_filterbank(n_fft, n_mels, sample_rate, wave.device)
+    spec = torch.stft(wave, n_fft=n_fft, hop_length=n_fft // 2, win_length=n_fft, window=win, center=True,
+                      pad_mode="reflect", normalized=False, onesided=True, return_complex=True)
+    return torch.matmul(spec.abs().pow(2.0).transpose(-1, -2), fb).transpose(-1, -2)

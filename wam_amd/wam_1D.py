@@ -118,6 +118,18 @@ class BaseWAM1D:
         grads = [v.detach().cpu().numpy() for v in plan.split(cg, n)]
         return g_mel.detach().cpu().numpy().squeeze(), grads
 
+    def filter(self, EPS):
+        """lib/wam_1D.py:221-246: keep the coefficients whose |gradient| / max(gradient) (signed
+        max over the band, as the reference) exceeds EPS and reconstruct (pywt.waverec ->
+        wam_waverec). Masks on the device; returns [N, rec_len] float32."""
+        if self._pass is None:
+            raise AttributeError("'BaseWAM1D' object has no attribute 'gradient_coeffs'")
+        plan, (cf, ci, c0), (gf, gi, g0), n = self._pass
+        cb = [v[c0:c0 + n] for v in plan.split(cf, ci)]
+        gb = [v[g0:g0 + n] for v in plan.split(gf, gi)]
+        flat = torch.cat([(c * ((g.abs() / g.max()) > EPS).float()).reshape(-1) for c, g in zip(cb, gb)])
+        return plan.waverec(flat, n)[0].cpu().numpy()
+
     def visualize_grad_wam(self, coeffs):
         """lib/wam_1D.py:152-192 (host numpy pseudo-scaleogram)."""
         batch = coeffs[0].shape[0]
@@ -247,3 +259,102 @@ class WaveletAttribution1D(BaseWAM1D):
             return self.smooth_wam(x, y)
         elif self.method == "integratedgrad":
             return self.integrated_wam(x, y)
+
+
+class VisualizerWAM1D(WaveletAttribution1D):
+    """lib/wam_1D.py:451-643: filtering of the explained waveforms by their attributions.
+
+    On the device: the wavelet-domain filters (hard threshold 'ht', soft 'st', scale-weighted
+    'modulation') on wam_wavedec / wam_waverec, the mel-spectrogram filters, the power mel
+    spectrogram. The reference's spectrograms come from librosa (absent offline, parity
+    unpinned): ``spectrogram_from_waveform`` restates librosa.stft's magnitude (hann window,
+    centred, constant padding -- librosa >= 0.10 -- hop n_fft // 4) with torch.stft on the GPU;
+    ``compute_spectrogram`` needs librosa's NNLS mel inversion (mel_to_stft) and raises
+    NotImplementedError, so ``filtered_spectrogram_from_melspec`` does too."""
+
+    def __init__(self, model, x, wavelet="haar", J=3, method="smooth", mode="reflect", device=None,
+                 approx_coeffs=False, n_mels=128, n_fft=1024, sample_rate=44100, n_samples=25, stdev_spread=0.001,
+                 random_seed=42, **kw):
+        super().__init__(model, wavelet, J, method, mode, device, approx_coeffs, n_mels, n_fft, sample_rate, n_samples,
+                         stdev_spread, random_seed, **kw)
+        self.source_spectrograms = None
+        self.x = x
+
+    def _wave(self, x):
+        if isinstance(x, list):
+            return _peak_normalise(x).to(self._dev)
+        return torch.as_tensor(np.asarray(x), dtype=torch.float32).to(self._dev)
+
+    def compute_melspec(self, x):
+        """power mel spectrograms [N, n_mels, frames] float32 (no dB), as the reference (:460-478)."""
+        from .melspec import melspec_power
+        return melspec_power(self._wave(x), self.n_fft, self.sample_rate, self.n_mels).cpu().numpy()
+
+    def compute_spectrogram(self, melspecs, chunk_size=100):
+        raise NotImplementedError("compute_spectrogram inverts mel spectrograms with librosa.feature.inverse."
+                                  "mel_to_stft (NNLS on librosa's own mel basis); librosa is not available")
+
+    def filter_melspec(self, audio_melspecs, grad_melspecs, filtering_method, EPS=0.2):
+        """lib/wam_1D.py:491-519 (hard threshold of the min-max-normalised gradient, or modulation)."""
+        a = torch.as_tensor(np.asarray(audio_melspecs)).to(self._dev)
+        g = torch.as_tensor(np.asarray(grad_melspecs)).to(self._dev).permute(0, 2, 1)
+        if filtering_method == "ht":
+            g = (g - g.min()) / (g.max() - g.min())
+            return (a * (g > EPS).to(a.dtype)).cpu().numpy()
+        elif filtering_method == "modulation":
+            return (a * g.abs()).cpu().numpy()
+        return None
+
+    def spectrogram_from_waveform(self, waveform):
+        """|librosa.stft(waveform, n_fft, hop_length=n_fft // 4)| (hann, centred, constant pad)."""
+        w = self._wave(waveform)
+        win = torch.hann_window(self.n_fft, device=w.device, dtype=w.dtype)
+        st = torch.stft(w, n_fft=self.n_fft, hop_length=self.n_fft // 4, win_length=self.n_fft, window=win,
+                        center=True, pad_mode="constant", return_complex=True)
+        return st.abs().cpu().numpy()
+
+    def _filtered_coeffs(self, coefficients, gradients, filtering_method="ht", EPS=0.2):
+        """wavelet-domain filters of :532-587 on device bands -> list of filtered bands."""
+        cs = [torch.as_tensor(np.asarray(c), dtype=torch.float32).to(self._dev) for c in coefficients]
+        gs = [torch.as_tensor(np.asarray(g), dtype=torch.float32).to(self._dev) for g in gradients]
+
+        def normalize(d):
+            return (d - d.min()) / (d.max() - d.min())
+        if filtering_method == "ht":
+            return [c * ((g.abs() / g.max()) > EPS).to(c.dtype) for c, g in zip(cs, gs)]
+        if filtering_method == "st":
+            return [c * torch.clamp(normalize(c * g) - EPS, min=0) for c, g in zip(cs, gs)]
+        if filtering_method == "modulation":
+            imp = torch.stack([g.sum(dim=1) for g in gs])                   # [levels, N]
+            nimp = (imp / imp.sum(dim=0, keepdim=True)).t()                 # [N, levels]
+            return [c * g.abs() * nimp[:, j:j + 1] for j, (c, g) in enumerate(zip(cs, gs))]
+        raise UnboundLocalError("local variable 'filtered_coeffs' referenced before assignment")
+
+    def filter_from_wavelet_coefficients(self, coefficients, gradients, filtering_method="ht", EPS=0.2):
+        """lib/wam_1D.py:532-587: filter in the wavelet domain, reconstruct (pywt.waverec ->
+        wam_waverec); returns [N, rec_len] float32."""
+        fc = self._filtered_coeffs(coefficients, gradients, filtering_method, EPS)
+        n = fc[0].shape[0]
+        from .filters import get_wavelet
+        L = len(get_wavelet(self.wavelet).dec_lo)
+        plan = get_plan(1, (2 * fc[-1].shape[-1] + 2 - L,), len(fc) - 1, self.wavelet, self.mode, self._dev)
+        return plan.waverec(torch.cat([c.reshape(-1) for c in fc]), n)[0].cpu().numpy()
+
+    def filtered_spectrogram_from_wavelet_coefficients(self, grad_coeffs, filtering_method, EPS=0.2):
+        """lib/wam_1D.py:589-617: spectrograms of x and of x filtered in the wavelet domain."""
+        x = np.asarray(self.x)
+        if x.dtype == np.int16:
+            x = np.array([wf / wf.max() for wf in self.x]).astype(np.float32)
+            self.x = x
+        self.source_spectrograms = self.spectrogram_from_waveform(x)
+        xd = torch.as_tensor(np.asarray(x), dtype=torch.float32).to(self._dev)
+        plan = get_plan(1, (xd.shape[-1],), self.J, self.wavelet, self.mode, self._dev)
+        coeffs = plan.split(plan.wavedec(xd.reshape(-1, xd.shape[-1])), xd.reshape(-1, xd.shape[-1]).shape[0])
+        sounds = self.filter_from_wavelet_coefficients(coeffs, grad_coeffs, filtering_method=filtering_method, EPS=EPS)
+        return self.source_spectrograms, self.spectrogram_from_waveform(sounds)
+
+    def filtered_spectrogram_from_melspec(self, grad_melspecs, filtering_method, EPS=0.2, chunk_size=100):
+        audio = self.compute_melspec(self.x)
+        self.source_spectrograms = self.compute_spectrogram(audio, chunk_size=chunk_size)
+        return self.source_spectrograms, self.compute_spectrogram(
+            self.filter_melspec(audio, grad_melspecs, filtering_method, EPS=EPS), chunk_size=chunk_size)
