@@ -274,6 +274,26 @@ int wam_visualize3d(int64_t items, int size, int levels, const float* cube, floa
                     void* stream);
 
 /* ------------------------------------------------------------------------------------------------
+ * 1D mel front-end (replaces lib/wam_1D.py:194-219, BaseWAM1D.compute_melspec: torchaudio
+ * MelSpectrogram(sample_rate, n_fft, n_mels) with its defaults -- periodic Hann, hop n_fft / 2,
+ * center + reflect padding, power 2, HTK mel without normalisation -- followed by AmplitudeToDB()
+ * when to_db, and the gradient torch autograd takes through it).
+ * wave [items, samples] float32 (samples > n_fft / 2); out / grad_out [items, F, n_mels] with
+ * F = samples / (n_fft / 2) + 1 (the reference's [N, 1, F, n_mels] stack); n_fft a power of two
+ * in [64, 4096] (WAM_ERR_UNSUPPORTED otherwise).
+ * tables (float, device): window[n_fft] | twiddle[2 n_fft] (cos, sin of -2 pi m / n_fft) |
+ *   band_w[nnz] | bin_w[nnz];
+ * index (int32, device): band_ptr[n_mels + 1] | band_bin[nnz] | bin_ptr[n_fft / 2 + 2] |
+ *   bin_band[nnz] -- the filterbank's nonzeros by band (bins ascending) and by bin (bands
+ *   ascending); wam_amd/melspec.py (MelTables) builds them from torchaudio's filterbank formula.
+ * grad_wave is written (not accumulated). */
+int wam_melspec(int64_t items, int64_t samples, int n_fft, int n_mels, int nnz, int to_db, const float* wave,
+                const float* tables, const int32_t* index, float* out, void* stream);
+int wam_melspec_adjoint(int64_t items, int64_t samples, int n_fft, int n_mels, int nnz, int to_db,
+                        const float* wave, const float* grad_out, const float* tables, const int32_t* index,
+                        float* grad_wave, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
  * Explained-model input-gradient pass (lib/wam_2D.py:114-116: model forward, diag-mean loss,
  * backward). Not a ptwt replacement: fused elementwise steps of a BN-folded ReLU network, each one
  * HBM pass instead of the 2-4 torch kernels it replaces (wam_amd/model_fuse.py drives them).

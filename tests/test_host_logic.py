@@ -177,3 +177,33 @@ def test_philox_known_answers():
     for ctr, key, want in kat:
         got = philox4x32_10(*[np.array([v]) for v in ctr], *key)
         assert tuple(int(v[0]) for v in got) == want
+
+
+def test_mel_tables_csr_matches_filterbank():
+    """MelTables (the tables k_mel_fwd / k_mel_adj read): both CSR forms rebuild the dense
+    filterbank, bins ascending within a band and bands ascending within a bin; twiddles/window."""
+    from wam_amd.melspec import MelTables, mel_filterbank
+    for n_fft, n_mels, sr in [(1024, 128, 16000), (1024, 128, 44100), (256, 40, 8000)]:
+        t = MelTables(n_fft, n_mels, sr, "cpu")
+        fb, win = mel_filterbank(n_fft, n_mels, sr, "cpu")
+        tab, idx = t.tables.numpy(), t.index.numpy()
+        nf, nnz, M = n_fft // 2 + 1, t.nnz, n_fft // 2
+        band_ptr = idx[:n_mels + 1]
+        band_bin = idx[n_mels + 1:n_mels + 1 + nnz]
+        bin_ptr = idx[n_mels + 1 + nnz:n_mels + 1 + nnz + M + 2]
+        bin_band = idx[n_mels + 1 + nnz + M + 2:]
+        band_w, bin_w = tab[3 * n_fft:3 * n_fft + nnz], tab[3 * n_fft + nnz:]
+        assert len(bin_band) == nnz and len(bin_w) == nnz
+        d1, d2 = np.zeros((nf, n_mels), np.float32), np.zeros((nf, n_mels), np.float32)
+        for m in range(n_mels):
+            bins = band_bin[band_ptr[m]:band_ptr[m + 1]]
+            assert np.all(np.diff(bins) > 0)
+            d1[bins, m] = band_w[band_ptr[m]:band_ptr[m + 1]]
+        for k in range(nf):
+            bands = bin_band[bin_ptr[k]:bin_ptr[k + 1]]
+            assert np.all(np.diff(bands) > 0)
+            d2[k, bands] = bin_w[bin_ptr[k]:bin_ptr[k + 1]]
+        assert np.array_equal(d1, fb.numpy()) and np.array_equal(d2, fb.numpy())
+        assert np.array_equal(tab[:n_fft], win.numpy())
+        tw = tab[n_fft:3 * n_fft].reshape(-1, 2)
+        assert np.allclose(tw[:, 0] + 1j * tw[:, 1], np.exp(-2j * np.pi * np.arange(n_fft) / n_fft), atol=1e-7)

@@ -64,6 +64,8 @@ _SIGS = {
     "wam_timing_enable": (c_int, [c_int]),
     "wam_copy": (c_int, [c_i64, c_vp, c_vp, c_vp]),
     "wam_visualize3d": (c_int, [c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "wam_melspec": (c_int, [c_i64, c_i64, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "wam_melspec_adjoint": (c_int, [c_i64, c_i64, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "wam_rank_masks": (c_int, [c_i64, c_i64, c_i64, c_vp, c_int, c_vp, c_vp]),
     "wam_coeff_masks": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "wam_quantize_normalize": (c_int, [c_i64, c_int, c_i64, c_vp, ctypes.POINTER(c_f32), ctypes.POINTER(c_f32),

@@ -12,7 +12,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libwam_hip.so")
-SOURCES = ["plan.hip", "dwt_axis.hip", "dwt2_fused.hip", "dwt2_rows.hip", "dwt2_plane.hip", "dwt1_tile.hip", "dwt3_haar.hip", "epilogue.hip", "evaluate.hip", "visualize3d.hip", "model_ew.hip"]
+SOURCES = ["plan.hip", "dwt_axis.hip", "dwt2_fused.hip", "dwt2_rows.hip", "dwt2_plane.hip", "dwt1_tile.hip", "dwt3_haar.hip", "epilogue.hip", "evaluate.hip", "visualize3d.hip", "melspec.hip", "model_ew.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("WAM_OFFLOAD_ARCH", "gfx950")
 

@@ -1,0 +1,590 @@
+// The 1D mel front-end (lib/wam_1D.py:194-219: torchaudio MelSpectrogram(sample_rate, n_fft,
+// n_mels) + AmplitudeToDB() per waveform) and its adjoint, one wave per frame.
+//
+// Frame f of a [T] waveform covers samples (f - 1) * hop + n, n < N (N = n_fft, hop = N / 2,
+// center=True, reflect padding), F = T / hop + 1 frames. Per frame:
+//   z[n] = x[2n] w[2n] + i x[2n+1] w[2n+1]   (periodic Hann w; the real frame packed in M = N/2
+//                                               complex points)
+//   Z = FFT_M(z)                              (in-place Stockham in the wave's LDS, radix 8 stages
+//                                               plus one radix 2/4 stage, table twiddles)
+//   X[k] = (Z[k] + conj Z[M-k]) / 2 - i/2 e^{-2 pi i k/N} (Z[k] - conj Z[M-k]),  k = 0..M
+//   P[k] = |X[k]|^2,  mel[m] = sum_k P[k] fb[k][m] (band-sparse),  db = 10 log10(max(mel, 1e-10))
+// The adjoint (what torch autograd does through stft -> abs -> pow -> matmul -> clamp -> log10)
+// recomputes the frame, forms G[k] = 2 dL/dP[k] X[k] and evaluates
+//   g_frame[n] = w[n] Re(sum_{k=0..M} G[k] e^{+2 pi i k n/N})
+// with one inverse M-point FFT of the Hermitian-packed spectrum; the reflect padding is folded
+// back when the frames are overlap-added. Workgroups own runs of hop-blocks of the output and keep
+// the frames touching them in LDS, so every output sample is written once, in a fixed order.
+//
+// tables (device, float): window[N] | twiddle[2N] (cos, sin of -2 pi m / N) | band_w[nnz] | bin_w[nnz]
+// index  (device, int32): band_ptr[n_mels+1] | band_bin[nnz] | bin_ptr[N/2+2] | bin_band[nnz]
+// (the filterbank's nonzeros by band and by bin, built on the host from torchaudio's HTK
+// filterbank: wam_amd/melspec.py).
+#include "kernels.hpp"
+
+#include <algorithm>
+#include <mutex>
+#include <set>
+
+namespace {
+
+constexpr int kWavesF = 4;  // forward: waves per workgroup, each streaming frames (one frame per wave at a time)
+constexpr int kWavesA = 8;  // adjoint: waves per workgroup sharing the run's frame slots
+
+struct MelGeom {
+  int64_t items, T;
+  int F, hop, n_mels, nnz;
+  int blocks_per_wg, wg_per_item;  // adjoint
+  int to_db;
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+// v * (S i)
+template <int S>
+__device__ __forceinline__ float2 muls(float2 v) {
+  return S < 0 ? make_float2(v.y, -v.x) : make_float2(-v.y, v.x);
+}
+
+// LDS index padding: breaks the stride-R writes of the first stages across banks
+__device__ __forceinline__ int pad(int i) { return i + (i >> 4); }
+
+template <int S>
+__device__ __forceinline__ void dft2(float2* a) {
+  const float2 t = a[0];
+  a[0] = cadd(t, a[1]);
+  a[1] = csub(t, a[1]);
+}
+
+template <int S>
+__device__ __forceinline__ void dft4(float2* a) {
+  const float2 c0 = cadd(a[0], a[2]), c2 = csub(a[0], a[2]);
+  const float2 c1 = cadd(a[1], a[3]), c3 = muls<S>(csub(a[1], a[3]));
+  a[0] = cadd(c0, c1);
+  a[1] = cadd(c2, c3);
+  a[2] = csub(c0, c1);
+  a[3] = csub(c2, c3);
+}
+
+template <int S>
+__device__ __forceinline__ void dft8(float2* a) {
+  constexpr float c = 0.70710678118654752f;
+  float2 b[8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    b[q] = cadd(a[q], a[q + 4]);
+    b[q + 4] = csub(a[q], a[q + 4]);
+  }
+  b[5] = cmul(b[5], make_float2(c, S * c));
+  b[6] = muls<S>(b[6]);
+  b[7] = cmul(b[7], make_float2(-c, S * c));
+  const float2 c0 = cadd(b[0], b[2]), c2 = csub(b[0], b[2]);
+  const float2 c1 = cadd(b[1], b[3]), c3 = muls<S>(csub(b[1], b[3]));
+  a[0] = cadd(c0, c1);
+  a[4] = csub(c0, c1);
+  a[2] = cadd(c2, c3);
+  a[6] = csub(c2, c3);
+  const float2 d0 = cadd(b[4], b[6]), d2 = csub(b[4], b[6]);
+  const float2 d1 = cadd(b[5], b[7]), d3 = muls<S>(csub(b[5], b[7]));
+  a[1] = cadd(d0, d1);
+  a[5] = csub(d0, d1);
+  a[3] = cadd(d2, d3);
+  a[7] = csub(d2, d3);
+}
+
+// stage plan of an M = 2^LOGM point FFT: one radix 2^(LOGM % 3) stage first (if any), then radix 8
+template <int LOGM>
+struct Plan {
+  static constexpr int first = LOGM % 3;  // log2 radix of the optional first stage
+  static constexpr int stages = LOGM / 3 + (first ? 1 : 0);
+  static constexpr int log_radix(int st) { return (first && st == 0) ? first : 3; }
+  static constexpr int log_ns(int st) { return st == 0 ? 0 : log_ns(st - 1) + log_radix(st - 1); }
+};
+
+// one in-place Stockham stage: all of a lane's butterflies are loaded before any is written back
+template <int LOGN, int ST, int S>
+__device__ __forceinline__ void fft_stage(float2* buf, const float2* __restrict__ tw, int lane) {
+  constexpr int LOGM = LOGN - 1, M = 1 << LOGM;
+  constexpr int LR = Plan<LOGM>::log_radix(ST), R = 1 << LR;
+  constexpr int LNS = Plan<LOGM>::log_ns(ST), Ns = 1 << LNS;
+  constexpr int B = M / R, NB = (B + 63) / 64;
+  float2 v[NB][R];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int j = lane + 64 * b;
+    if (B % 64 == 0 || j < B) {
+      const int k = j & (Ns - 1);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        float2 x = buf[pad(j + r * B)];
+        if (Ns > 1 && r > 0) {
+          float2 t = tw[(r * k) << (LOGN - LNS - LR)];
+          if (S > 0) t = cconj(t);
+          x = cmul(x, t);
+        }
+        v[b][r] = x;
+      }
+      if (R == 8) dft8<S>(v[b]);
+      else if (R == 4) dft4<S>(v[b]);
+      else dft2<S>(v[b]);
+    }
+  }
+  wave_sync();
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int j = lane + 64 * b;
+    if (B % 64 == 0 || j < B) {
+      const int k = j & (Ns - 1);
+      const int idx = ((j >> LNS) << (LNS + LR)) + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) buf[pad(idx + r * Ns)] = v[b][r];
+    }
+  }
+  wave_sync();
+}
+
+template <int LOGN, int ST, int S>
+__device__ __forceinline__ void fft_stages(float2* buf, const float2* __restrict__ tw, int lane) {
+  if constexpr (ST < Plan<LOGN - 1>::stages) {
+    fft_stage<LOGN, ST, S>(buf, tw, lane);
+    fft_stages<LOGN, ST + 1, S>(buf, tw, lane);
+  }
+}
+
+// the kernels' constant tables: staged in LDS once per workgroup (n_fft <= 1024), else read from
+// global memory (L1/L2-resident)
+struct Tabs {
+  const float* win;
+  const float2* tw;
+  const float* band_w;
+  const float* bin_w;
+  const int* band_ptr;
+  const int* band_bin;
+  const int* bin_ptr;
+  const int* bin_band;
+};
+
+__host__ __device__ inline int tab_floats(int N, int n_mels, int nnz, bool adj) {
+  const int nf = 3 * N + nnz * (adj ? 2 : 1);
+  const int ni = n_mels + 1 + nnz + (adj ? N / 2 + 2 + nnz : 0);
+  return (nf + ni + 3) & ~3;  // float4-aligned end
+}
+
+template <bool STAGE>
+__device__ __forceinline__ Tabs stage_tables(const MelGeom& g, int N, const float* __restrict__ tables,
+                                             const int* __restrict__ index, float* lds, bool adj) {
+  const int nf = 3 * N + g.nnz * (adj ? 2 : 1);
+  const int ni = g.n_mels + 1 + g.nnz + (adj ? N / 2 + 2 + g.nnz : 0);
+  const float* tf = tables;
+  const int* ti = index;
+  if (STAGE) {
+    for (int i = threadIdx.x; i < nf; i += blockDim.x) lds[i] = tables[i];
+    int* li = reinterpret_cast<int*>(lds + nf);
+    for (int i = threadIdx.x; i < ni; i += blockDim.x) li[i] = index[i];
+    __syncthreads();
+    tf = lds;
+    ti = li;
+  }
+  Tabs t;
+  t.win = tf;
+  t.tw = reinterpret_cast<const float2*>(tf + N);
+  t.band_w = tf + 3 * N;
+  t.bin_w = t.band_w + g.nnz;
+  t.band_ptr = ti;
+  t.band_bin = ti + g.n_mels + 1;
+  t.bin_ptr = t.band_bin + g.nnz;
+  t.bin_band = t.bin_ptr + N / 2 + 2;
+  return t;
+}
+
+// a frame's samples held in registers: fetched one frame ahead, stored (windowed) into the
+// wave's LDS buffer when its turn comes
+template <int LOGN>
+struct FrameIn {
+  static constexpr int M = 1 << (LOGN - 1), KM = (M + 63) / 64;
+  float a[KM], b[KM];
+
+  __device__ __forceinline__ void fetch(const float* __restrict__ x, int64_t T, int f, int hop, int F, int lane) {
+    const int64_t s0 = (int64_t)(f - 1) * hop;
+    if (f > 0 && f < F - 1) {
+      if ((reinterpret_cast<uintptr_t>(x) & 7) == 0) {  // s0 is even: aligned float2 pairs
+        const float2* x2 = reinterpret_cast<const float2*>(x + s0);
+#pragma unroll
+        for (int i = 0; i < KM; ++i) {
+          const int n = lane + 64 * i;
+          if (M % 64 == 0 || n < M) {
+            const float2 v = x2[n];
+            a[i] = v.x;
+            b[i] = v.y;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < KM; ++i) {
+          const int n = lane + 64 * i;
+          if (M % 64 == 0 || n < M) {
+            a[i] = x[s0 + 2 * n];
+            b[i] = x[s0 + 2 * n + 1];
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < KM; ++i) {
+        const int n = lane + 64 * i;
+        if (M % 64 == 0 || n < M) {
+          int64_t s = s0 + 2 * n, t = s + 1;
+          s = s < 0 ? -s : (s >= T ? 2 * (T - 1) - s : s);
+          t = t < 0 ? -t : (t >= T ? 2 * (T - 1) - t : t);
+          a[i] = x[s];
+          b[i] = x[t];
+        }
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(const float* win, float2* buf, int lane) const {
+#pragma unroll
+    for (int i = 0; i < KM; ++i) {
+      const int n = lane + 64 * i;
+      if (M % 64 == 0 || n < M) buf[pad(n)] = make_float2(a[i] * win[2 * n], b[i] * win[2 * n + 1]);
+    }
+  }
+};
+
+// X[k] of bin k (k <= M) from the packed spectrum in buf
+template <int LOGN>
+__device__ __forceinline__ float2 unpack_bin(const float2* buf, const float2* tw, int k) {
+  constexpr int M = 1 << (LOGN - 1);
+  const float2 zk = buf[pad(k & (M - 1))], zc = cconj(buf[pad((M - k) & (M - 1))]);
+  const float2 e = make_float2(0.5f * (zk.x + zc.x), 0.5f * (zk.y + zc.y));
+  const float2 d = csub(zk, zc);
+  const float2 o = make_float2(0.5f * d.y, -0.5f * d.x);  // -i/2 (zk - zc)
+  return cadd(e, cmul(tw[k], o));
+}
+
+// FFT of the stored frame, then P[k] = |X[k]|^2 into buf (as floats, k <= M); X kept if asked
+template <int LOGN, bool KEEP>
+__device__ __forceinline__ void frame_power(const Tabs& t, float2* buf, float2* X, int lane) {
+  constexpr int M = 1 << (LOGN - 1), KI = M / 64 + 1;
+  fft_stages<LOGN, 0, -1>(buf, t.tw, lane);
+  float p[KI];
+#pragma unroll
+  for (int i = 0; i < KI; ++i) {
+    const int k = lane + 64 * i;
+    if (k <= M) {
+      const float2 x = unpack_bin<LOGN>(buf, t.tw, k);
+      if (KEEP) X[i] = x;
+      p[i] = x.x * x.x + x.y * x.y;
+    }
+  }
+  wave_sync();
+  float* P = reinterpret_cast<float*>(buf);
+#pragma unroll
+  for (int i = 0; i < KI; ++i)
+    if (lane + 64 * i <= M) P[lane + 64 * i] = p[i];
+  wave_sync();
+}
+
+__device__ __forceinline__ float band_sum(const Tabs& t, const float* P, int m) {
+  float acc = 0.f;
+  const int e1 = t.band_ptr[m + 1];
+#pragma unroll 4
+  for (int e = t.band_ptr[m]; e < e1; ++e) acc = fmaf(P[t.band_bin[e]], t.band_w[e], acc);
+  return acc;
+}
+
+template <int LOGN, bool STAGE>
+__global__ void __launch_bounds__(64 * kWavesF) k_mel_fwd(MelGeom g, const float* __restrict__ wave,
+                                                          const float* __restrict__ tables,
+                                                          const int* __restrict__ index, float* __restrict__ out) {
+  constexpr int N = 1 << LOGN, M = N / 2;
+  extern __shared__ float4 lds_raw[];
+  float* lf = reinterpret_cast<float*>(lds_raw);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const Tabs t = stage_tables<STAGE>(g, N, tables, index, lf, false);
+  float2* buf = reinterpret_cast<float2*>(lf + (STAGE ? tab_floats(N, g.n_mels, g.nnz, false) : 0)) + w * (pad(M) + 2);
+  const int64_t frames = g.items * g.F, stride = (int64_t)gridDim.x * kWavesF;
+  int64_t q = (int64_t)blockIdx.x * kWavesF + w;
+  FrameIn<LOGN> in;
+  if (q < frames) in.fetch(wave + (q / g.F) * g.T, g.T, (int)(q % g.F), g.hop, g.F, lane);
+  for (; q < frames; q += stride) {
+    in.store(t.win, buf, lane);
+    const int64_t qn = q + stride;
+    if (qn < frames) in.fetch(wave + (qn / g.F) * g.T, g.T, (int)(qn % g.F), g.hop, g.F, lane);
+    wave_sync();
+    frame_power<LOGN, false>(t, buf, nullptr, lane);
+    const float* P = reinterpret_cast<const float*>(buf);
+    float* o = out + q * g.n_mels;
+    for (int m = lane; m < g.n_mels; m += 64) {
+      const float acc = band_sum(t, P, m);
+      o[m] = g.to_db ? 10.f * log10f(fmaxf(acc, 1e-10f)) : acc;
+    }
+    wave_sync();
+  }
+}
+
+// one frame's gradient g_frame[N] into slot (the whole adjoint chain of the frame, see header);
+// the frame's samples are in `in`, which is refilled with frame f_next (if >= 0) meanwhile
+template <int LOGN>
+__device__ void frame_adjoint(const MelGeom& g, const Tabs& t, FrameIn<LOGN>& in, const float* __restrict__ x,
+                              int f, int f_next, const float* __restrict__ gdb, float2* buf, float* gmel, float* slot,
+                              int lane) {
+  constexpr int M = 1 << (LOGN - 1), KI = M / 64 + 1;
+  constexpr int kMelRegs = 4;  // bands lane + 64 j, j < 4, held in registers (n_mels <= 256)
+  in.store(t.win, buf, lane);
+  if (f_next >= 0) in.fetch(x, g.T, f_next, g.hop, g.F, lane);
+  float gq[kMelRegs];
+  const float* gf = gdb + (int64_t)f * g.n_mels;
+#pragma unroll
+  for (int j = 0; j < kMelRegs; ++j) gq[j] = lane + 64 * j < g.n_mels ? gf[lane + 64 * j] : 0.f;
+  wave_sync();
+  float2 X[KI];
+  frame_power<LOGN, true>(t, buf, X, lane);
+  const float* P = reinterpret_cast<const float*>(buf);
+  // d db / d mel: mul(10) -> log10 -> clamp(min=1e-10), in torch's order
+#pragma unroll
+  for (int j = 0; j < kMelRegs; ++j) {
+    const int m = lane + 64 * j;
+    if (m < g.n_mels) {
+      const float acc = band_sum(t, P, m);
+      float gm = gq[j];
+      if (g.to_db) {
+        const float gl = gm * 10.f;
+        gm = acc >= 1e-10f ? gl / (fmaxf(acc, 1e-10f) * 2.302585092994046f) : 0.f;
+      }
+      gmel[m] = gm;
+    }
+  }
+  wave_sync();
+  // A[k] = 2 dL/dP[k] X[k] (real at k = 0, M: doubled real part, the Hermitian pair folded)
+  float2 A[KI];
+#pragma unroll
+  for (int i = 0; i < KI; ++i) {
+    const int k = lane + 64 * i;
+    if (k <= M) {
+      float gp = 0.f;
+      const int e1 = t.bin_ptr[k + 1];
+      for (int e = t.bin_ptr[k]; e < e1; ++e) gp = fmaf(gmel[t.bin_band[e]], t.bin_w[e], gp);
+      A[i] = make_float2(2.f * gp * X[i].x, 2.f * gp * X[i].y);
+      if (k == 0 || k == M) A[i] = make_float2(2.f * A[i].x, 0.f);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < KI; ++i)
+    if (lane + 64 * i <= M) buf[pad(lane + 64 * i)] = A[i];
+  wave_sync();
+  // Z''[k] = (A_k + conj A_{M-k}) + i (A_k - conj A_{M-k}) e^{+2 pi i k/N},  k < M
+  float2 Zp[KI];
+#pragma unroll
+  for (int i = 0; i < KI; ++i) {
+    const int k = lane + 64 * i;
+    if (k < M) {
+      const float2 ak = buf[pad(k)], ac = cconj(buf[pad(M - k)]);
+      const float2 d = cmul(csub(ak, ac), cconj(t.tw[k]));
+      const float2 s = cadd(ak, ac);
+      Zp[i] = make_float2(s.x - d.y, s.y + d.x);
+    }
+  }
+  wave_sync();
+#pragma unroll
+  for (int i = 0; i < KI; ++i)
+    if (lane + 64 * i < M) buf[pad(lane + 64 * i)] = Zp[i];
+  wave_sync();
+  fft_stages<LOGN, 0, 1>(buf, t.tw, lane);
+  float2* s2 = reinterpret_cast<float2*>(slot);
+  for (int n = lane; n < M; n += 64) {
+    const float2 z = buf[pad(n)];
+    s2[n] = make_float2(t.win[2 * n] * (0.5f * z.x), t.win[2 * n + 1] * (0.5f * z.y));
+  }
+  wave_sync();
+}
+
+// grid: wg_per_item x items workgroups; workgroup (c, it) owns hop-blocks [c * BPW, (c + 1) * BPW)
+template <int LOGN, bool STAGE>
+__global__ void __launch_bounds__(64 * kWavesA) k_mel_adj(MelGeom g, const float* __restrict__ wave,
+                                                          const float* __restrict__ gdb,
+                                                          const float* __restrict__ tables,
+                                                          const int* __restrict__ index, float* __restrict__ gwave) {
+  constexpr int N = 1 << LOGN, M = N / 2;
+  extern __shared__ float4 lds_raw[];
+  float* lf = reinterpret_cast<float*>(lds_raw);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int BPW = g.blocks_per_wg;
+  const Tabs t = stage_tables<STAGE>(g, N, tables, index, lf, true);
+  float* slots = lf + (STAGE ? tab_floats(N, g.n_mels, g.nnz, true) : 0);  // (BPW + 2) x N
+  float2* bufs = reinterpret_cast<float2*>(slots + (int64_t)(BPW + 2) * N);
+  float2* buf = bufs + w * (pad(M) + 2);
+  float* gmel = reinterpret_cast<float*>(bufs + kWavesA * (pad(M) + 2)) + w * g.n_mels;
+  const int64_t it = blockIdx.x / g.wg_per_item;
+  const int c = (int)(blockIdx.x - it * g.wg_per_item);
+  const int hop = g.hop, F = g.F;
+  const int64_t T = g.T;
+  const int b0 = c * BPW, b1 = b0 + BPW;
+  const int64_t s_lo = (int64_t)b0 * hop, s_hi = min((int64_t)b1 * hop, T);
+  const int f_hi = min(b1, F - 1);
+  const int nat = f_hi - b0 + 1;
+  // the last frame folds back onto [2T - 1 - F hop, T - 2]; a run ending just before it needs it too
+  const int64_t r_lo = 2 * T - 1 - (int64_t)F * hop;
+  const bool extra_last = f_hi < F - 1 && s_hi - 1 >= r_lo;
+  const int nframes = nat + (extra_last ? 1 : 0);
+  const float* x = wave + it * T;
+  const float* gd = gdb + it * (int64_t)F * g.n_mels;
+  FrameIn<LOGN> in;
+  if (w < nframes) in.fetch(x, T, w < nat ? b0 + w : F - 1, hop, F, lane);
+  for (int i = w; i < nframes; i += kWavesA) {
+    const int f = i < nat ? b0 + i : F - 1;
+    const int in_ = i + kWavesA;
+    const int f_next = in_ < nframes ? (in_ < nat ? b0 + in_ : F - 1) : -1;
+    frame_adjoint<LOGN>(g, t, in, x, f, f_next, gd, buf, gmel, slots + (int64_t)i * N, lane);
+  }
+  __syncthreads();
+  const int last_slot = extra_last ? nat : F - 1 - b0;  // slot of frame F - 1 if held
+  float* o = gwave + it * T;
+  for (int64_t s = s_lo + threadIdx.x; s < s_hi; s += blockDim.x) {
+    const int b = (int)(s / hop);
+    const int n = (int)(s - (int64_t)b * hop);
+    float acc = slots[(int64_t)(b - b0) * N + n + hop];  // frame b
+    if (b + 1 <= F - 1) acc += slots[(int64_t)(b + 1 - b0) * N + n];  // frame b + 1
+    if (s >= 1 && s <= hop) acc += slots[hop - s];  // frame 0 (b0 == 0 here), reflected
+    const int64_t se = 2 * (T - 1) - s;
+    if (se >= T && s >= r_lo) acc += slots[(int64_t)last_slot * N + (se - (int64_t)(F - 2) * hop)];
+    o[s] = acc;
+  }
+}
+
+constexpr int kMaxLds = 160 * 1024;
+
+int lds_fwd(int log_n, int n_mels, int nnz) {
+  const int N = 1 << log_n, M = N / 2;
+  return (log_n <= 10 ? tab_floats(N, n_mels, nnz, false) * 4 : 0) + kWavesF * (M + (M >> 4) + 2) * 8;
+}
+
+int lds_adj(int log_n, int bpw, int n_mels, int nnz) {
+  const int N = 1 << log_n, M = N / 2;
+  return (log_n <= 10 ? tab_floats(N, n_mels, nnz, true) * 4 : 0) + (bpw + 2) * N * 4 +
+         kWavesA * (M + (M >> 4) + 2) * 8 + kWavesA * n_mels * 4;
+}
+
+// hop-blocks per adjoint workgroup: 15 (16 frames = 2 per wave) when LDS allows, at least 2
+int blocks_per_wg(int log_n, int n_mels, int nnz) {
+  int bpw = 15;
+  while (bpw > 2 && lds_adj(log_n, bpw, n_mels, nnz) > kMaxLds) --bpw;
+  return bpw;
+}
+
+int lds_opt_in_mel(const void* kern, int bytes) {
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> done;
+  if (bytes <= 64 * 1024) return WAM_OK;
+  int dev = 0;
+  WAM_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  if (done.count({kern, dev})) return WAM_OK;
+  WAM_HIP_CHECK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  done.insert({kern, dev});
+  return WAM_OK;
+}
+
+int check_args(int64_t items, int64_t samples, int n_fft, int n_mels, int nnz, int* log_n) {
+  if (items < 0 || n_mels < 1 || nnz < 0) return WAM_ERR_INVALID_ARG;
+  int l = 0;
+  while ((1 << l) < n_fft) ++l;
+  if ((1 << l) != n_fft || l < 6 || l > 11 || n_mels > 256) return WAM_ERR_UNSUPPORTED;
+  if (nnz > 2 * (n_fft / 2 + 1)) return WAM_ERR_INVALID_ARG;  // a triangular bank: <= 2 bands per bin
+  if (samples <= n_fft / 2) return WAM_ERR_SHAPE;              // reflect pad needs T > n_fft / 2
+  *log_n = l;
+  return WAM_OK;
+}
+
+}  // namespace
+
+extern "C" int wam_melspec(int64_t items, int64_t samples, int n_fft, int n_mels, int nnz, int to_db,
+                           const float* wave, const float* tables, const int* index, float* out, void* stream) {
+  int log_n = 0;
+  if (int rc = check_args(items, samples, n_fft, n_mels, nnz, &log_n)) return rc;
+  if (items == 0) return WAM_OK;
+  if (!wave || !tables || !index || !out) return WAM_ERR_INVALID_ARG;
+  MelGeom g{};
+  g.items = items;
+  g.T = samples;
+  g.hop = n_fft / 2;
+  g.F = (int)(samples / g.hop + 1);
+  g.n_mels = n_mels;
+  g.nnz = nnz;
+  g.to_db = to_db ? 1 : 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t frames = items * g.F;
+  const int lds = lds_fwd(log_n, n_mels, nnz);
+  if (lds > kMaxLds) return WAM_ERR_UNSUPPORTED;
+  int cus = 256;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  // persistent-ish grid: a few workgroups per CU, each wave streaming frames with one-ahead prefetch
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((frames + kWavesF - 1) / kWavesF, 4 * cus));
+  WamTimer tm(st, "k_mel_fwd", 4.0 * (double)items * samples + 4.0 * (double)frames * n_mels);
+  switch (log_n) {
+#define WAM_MELF(L)                                                                                           \
+  case L:                                                                                                     \
+    if (int rc = lds_opt_in_mel((const void*)k_mel_fwd<L, (L <= 10)>, lds)) return rc;                        \
+    hipLaunchKernelGGL((k_mel_fwd<L, (L <= 10)>), dim3(grid), dim3(64 * kWavesF), lds, st, g, wave, tables, index, \
+                       out);                                                                                  \
+    break;
+    WAM_MELF(6) WAM_MELF(7) WAM_MELF(8) WAM_MELF(9) WAM_MELF(10) WAM_MELF(11)
+#undef WAM_MELF
+    default: return WAM_ERR_UNSUPPORTED;
+  }
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+extern "C" int wam_melspec_adjoint(int64_t items, int64_t samples, int n_fft, int n_mels, int nnz, int to_db,
+                                   const float* wave, const float* grad_out, const float* tables, const int* index,
+                                   float* grad_wave, void* stream) {
+  int log_n = 0;
+  if (int rc = check_args(items, samples, n_fft, n_mels, nnz, &log_n)) return rc;
+  if (items == 0) return WAM_OK;
+  if (!wave || !grad_out || !tables || !index || !grad_wave) return WAM_ERR_INVALID_ARG;
+  MelGeom g{};
+  g.items = items;
+  g.T = samples;
+  g.hop = n_fft / 2;
+  g.F = (int)(samples / g.hop + 1);
+  g.n_mels = n_mels;
+  g.nnz = nnz;
+  g.to_db = to_db ? 1 : 0;
+  const int nb = (int)((samples + g.hop - 1) / g.hop);
+  g.blocks_per_wg = blocks_per_wg(log_n, n_mels, nnz);
+  g.wg_per_item = (nb + g.blocks_per_wg - 1) / g.blocks_per_wg;
+  const int lds = lds_adj(log_n, g.blocks_per_wg, n_mels, nnz);
+  if (lds > kMaxLds) return WAM_ERR_UNSUPPORTED;
+  if (items * g.wg_per_item > 0x7fffffff) return WAM_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned grid = (unsigned)(items * g.wg_per_item);
+  WamTimer tm(st, "k_mel_adj", 8.0 * (double)items * samples + 4.0 * (double)items * g.F * n_mels);
+  switch (log_n) {
+#define WAM_MELA(L)                                                                                              \
+  case L:                                                                                                        \
+    if (int rc = lds_opt_in_mel((const void*)k_mel_adj<L, (L <= 10)>, lds)) return rc;                           \
+    hipLaunchKernelGGL((k_mel_adj<L, (L <= 10)>), dim3(grid), dim3(64 * kWavesA), lds, st, g, wave, grad_out, tables, \
+                       index, grad_wave);                                                                        \
+    break;
+    WAM_MELA(6) WAM_MELA(7) WAM_MELA(8) WAM_MELA(9) WAM_MELA(10) WAM_MELA(11)
+#undef WAM_MELA
+    default: return WAM_ERR_UNSUPPORTED;
+  }
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}

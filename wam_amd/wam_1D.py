@@ -13,7 +13,7 @@ import torch
 
 from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, legacy_noise, model_device,
                      require_gpu_device)
-from .melspec import melspec_db
+from .melspec import kernel_supported, mel_adjoint, mel_forward, melspec_db
 from .plan import accumulate_f32, get_plan, item_sigma, noise_add, trapz_stream
 
 
@@ -83,9 +83,14 @@ class BaseWAM1D:
         return self._grads_from_rec(plan, plan.waverec(flat, items)[0], y, groups, n)
 
     def _grads_from_rec(self, plan, rec, y, groups, n):
+        args = (self.n_fft, self.sample_rate, self.n_mels)
+        if kernel_supported(self.n_fft, self.n_mels):  # k_mel_fwd -> model -> k_mel_adj
+            mel = mel_forward(rec, *args).unsqueeze(1)
+            g_mel = input_gradient(self.model, mel, y, groups, n, self.autocast_dtype)
+            return g_mel, plan.adjoint(mel_adjoint(rec, g_mel, *args))
         rec_leaf = rec.detach().requires_grad_(True)
         with torch.enable_grad():
-            mel = melspec_db(rec_leaf, self.n_fft, self.sample_rate, self.n_mels)
+            mel = melspec_db(rec_leaf, *args)
         g_mel = input_gradient(self.model, mel.detach(), y, groups, n, self.autocast_dtype)
         (g_rec,) = torch.autograd.grad(mel, rec_leaf, grad_outputs=g_mel)
         return g_mel, plan.adjoint(g_rec.contiguous())
