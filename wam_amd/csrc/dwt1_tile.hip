@@ -16,10 +16,13 @@
 #include <algorithm>
 #include <mutex>
 #include <set>
+#include <type_traits>
 
 #include "kernels.hpp"
 
 namespace {
+
+typedef float f2v __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_fma_f32)
 
 // opt in to more than 64 KB of dynamic LDS, once per (kernel, device)
 int lds_opt_in(const void* kern, int bytes) {
@@ -103,40 +106,18 @@ __host__ __device__ __forceinline__ void ana_ranges(const Dwt1Geom& g, int tile,
   }
 }
 
-// tiles [t_lo, t_hi) are left to k_dwt1_ana_int; this kernel runs the others (nb per signal)
+// the J levels of one tile from its source window in smem[0, wlen) (extension applied on the
+// load): level 0 from the window, levels 1..J-1 from two approximation buffers after it
 template <int L>
-__global__ void __launch_bounds__(kT1) k_dwt1_ana(const float* __restrict__ in, float* __restrict__ coeffs,
-                                                 const float* __restrict__ filt, Dwt1Geom g, int t_lo, int t_hi) {
+__device__ __forceinline__ void ana_tile_levels(float* smem, const float* flo, const float* fhi, const Dwt1Geom& g,
+                                                float* __restrict__ coeffs, int64_t item, const int* S,
+                                                const int* E, const int* s, const int* e) {
   constexpr int p = L - 2;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
-  const int nb = g.tiles - (t_hi - t_lo);
-  const int64_t item = blockIdx.x / nb;
-  const int kb = (int)(blockIdx.x % nb);
-  const int tile = kb < t_lo ? kb : t_hi + (kb - t_lo);
-  float flo[L], fhi[L];
-#pragma unroll
-  for (int k = 0; k < L; ++k) {
-    flo[k] = filt[k];
-    fhi[k] = filt[L + k];
-  }
-  __shared__ int S[WAM_MAX_LEVELS], E[WAM_MAX_LEVELS], s[WAM_MAX_LEVELS], e[WAM_MAX_LEVELS];
-  if (tid == 0) ana_ranges(g, tile, p, S, E, s, e);
-  __syncthreads();
   const int J = g.J, mode = g.mode;
-  // LDS (offsets into smem, so every access stays an LDS instruction): source window, then two
-  // approximation buffers. Window = extended indices [2 S0 - p, 2 E0 - 1) of the input.
-  const int w0 = 2 * S[0] - p;
   const int wlen = 2 * (E[0] - S[0]) + L - 2;
   const int off_ll0 = (wlen + 63) & ~63;
   const int off_ll1 = off_ll0 + ((E[0] - S[0] + 63) & ~63);
-  const float* x = in + item * (int64_t)g.n;
-  for (int j = tid; j < wlen; j += kT1) {
-    const int si = ext_near(w0 + j, g.n, mode);
-    smem[j] = si >= 0 ? x[si] : 0.f;
-  }
-  __syncthreads();
-  // level 0 from the window (extension already applied)
   {
     const int ml = g.m[0];
     const bool last = J == 1;
@@ -199,6 +180,101 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana(const float* __restrict__ in, 
   }
 }
 
+// tiles [t_lo, t_hi) are left to k_dwt1_ana_int; this kernel runs the others (nb per signal)
+template <int L>
+__global__ void __launch_bounds__(kT1) k_dwt1_ana(const float* __restrict__ in, float* __restrict__ coeffs,
+                                                 const float* __restrict__ filt, Dwt1Geom g, int t_lo, int t_hi) {
+  constexpr int p = L - 2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int nb = g.tiles - (t_hi - t_lo);
+  const int64_t item = blockIdx.x / nb;
+  const int kb = (int)(blockIdx.x % nb);
+  const int tile = kb < t_lo ? kb : t_hi + (kb - t_lo);
+  float flo[L], fhi[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    flo[k] = filt[k];
+    fhi[k] = filt[L + k];
+  }
+  __shared__ int S[WAM_MAX_LEVELS], E[WAM_MAX_LEVELS], s[WAM_MAX_LEVELS], e[WAM_MAX_LEVELS];
+  if (tid == 0) ana_ranges(g, tile, p, S, E, s, e);
+  __syncthreads();
+  // window = extended indices [2 S0 - p, 2 E0 - 1) of the input
+  const int w0 = 2 * S[0] - p;
+  const int wlen = 2 * (E[0] - S[0]) + L - 2;
+  const float* x = in + item * (int64_t)g.n;
+  for (int j = tid; j < wlen; j += kT1) {
+    const int si = ext_near(w0 + j, g.n, g.mode);
+    smem[j] = si >= 0 ? x[si] : 0.f;
+  }
+  __syncthreads();
+  ana_tile_levels<L>(smem, flo, fhi, g, coeffs, item, S, E, s, e);
+}
+
+// the same boundary tiles, persistent: workgroups loop over (signal, boundary tile) units and fetch
+// the next unit's window (extension applied) into registers while the current unit's levels run;
+// used when every boundary window fits kPF floats per thread
+constexpr int kPF = 20;  // window floats prefetched per thread (window <= kPF * kT1)
+
+template <int L>
+__global__ void __launch_bounds__(kT1) k_dwt1_ana_p(const float* __restrict__ in, float* __restrict__ coeffs,
+                                                   const float* __restrict__ filt, Dwt1Geom g, int t_lo, int t_hi,
+                                                   int64_t units) {
+  constexpr int p = L - 2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int nb = g.tiles - (t_hi - t_lo);
+  float flo[L], fhi[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    flo[k] = filt[k];
+    fhi[k] = filt[L + k];
+  }
+  __shared__ int R[2][4][WAM_MAX_LEVELS];  // (S, E, s, e) of the current and the next unit
+  auto ranges = [&](int64_t u, int slot) {
+    const int kb = (int)(u % nb);
+    ana_ranges(g, kb < t_lo ? kb : t_hi + (kb - t_lo), p, R[slot][0], R[slot][1], R[slot][2], R[slot][3]);
+  };
+  float pf[kPF];
+  uint32_t zmask = 0;  // window slots that are zeros (zero-mode extension): applied when stored, so
+                       // the loads themselves stay unconditional and all in flight together
+  auto prefetch = [&](int64_t u, int slot) {
+    const int64_t item = u / nb;
+    const int w0 = 2 * R[slot][0][0] - p;
+    const int wlen = 2 * (R[slot][1][0] - R[slot][0][0]) + L - 2;
+    const float* x = in + item * (int64_t)g.n;
+    zmask = 0;
+#pragma unroll
+    for (int r = 0; r < kPF; ++r) {
+      const int j = tid + r * kT1;
+      const int si = j < wlen ? ext_near(w0 + j, g.n, g.mode) : -1;
+      zmask |= (si < 0 ? 1u : 0u) << r;
+      pf[r] = x[si >= 0 ? si : 0];
+    }
+  };
+  int64_t u = blockIdx.x;
+  int cur = 0;
+  if (u < units) {
+    if (tid == 0) ranges(u, 0);
+    __syncthreads();
+    prefetch(u, 0);
+  }
+  for (; u < units; u += gridDim.x) {
+    const int wlen = 2 * (R[cur][1][0] - R[cur][0][0]) + L - 2;
+#pragma unroll
+    for (int r = 0; r < kPF; ++r) {
+      const int j = tid + r * kT1;
+      if (j < wlen) smem[j] = (zmask >> r) & 1u ? 0.f : pf[r];
+    }
+    const int64_t un = u + gridDim.x;
+    if (tid == 0 && un < units) ranges(un, cur ^ 1);
+    __syncthreads();
+    if (un < units) prefetch(un, cur ^ 1);  // in flight while the levels run
+    ana_tile_levels<L>(smem, flo, fhi, g, coeffs, u / nb, R[cur][0], R[cur][1], R[cur][2], R[cur][3]);
+    cur ^= 1;
+  }
+}
 
 // ------------------------------------------------------------------------------------------------
 // Interior tiles (no boundary extension at any level): persistent workgroups over (signal, tile)
@@ -208,7 +284,6 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana(const float* __restrict__ in, 
 // output r reads E[r + m], O[r + m]: consecutive lanes hit consecutive banks and the taps keep the
 // k = 0..L-1 fma order of the per-axis kernels (same sums). The next unit's window is fetched into
 // registers before the current unit's levels run, hiding its HBM latency.
-constexpr int kPF = 20;          // window floats prefetched per thread (window <= kPF * kT1)
 
 __host__ __device__ __forceinline__ int eo_cap(int n) { return (((n + 1) / 2 + 31) & ~31) + 16; }
 
@@ -280,22 +355,49 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ 
       const int own0 = tile * T;
       float* dout = coeffs + g.items * g.off_d[l] + item * (int64_t)ml;
       float* aout = coeffs + g.items * g.off_a + item * (int64_t)ml;
-      for (int r = tid; r < nl; r += kT1) {
-        float a = 0.f, d = 0.f;
+      // output pair (r, r + 1), r even: E/O[r .. r + H2] read once as float2, both outputs'
+      // lo / hi sums as packed fp32 fma (per-output tap order unchanged)
+      constexpr int H2 = L / 2, NP = H2 / 2 + 1;
+      const bool dpair = ((reinterpret_cast<uintptr_t>(dout + Sl) | reinterpret_cast<uintptr_t>(aout + Sl)) & 7) == 0;
+      for (int r = 2 * tid; r < nl; r += 2 * kT1) {
+        float e[2 * NP], o[2 * NP];
 #pragma unroll
-        for (int m2 = 0; m2 < L / 2; ++m2) {
-          const float ve = iE[r + m2], vo = iO[r + m2];
-          a = fmaf(flo[2 * m2], ve, a);
-          d = fmaf(fhi[2 * m2], ve, d);
-          a = fmaf(flo[2 * m2 + 1], vo, a);
-          d = fmaf(fhi[2 * m2 + 1], vo, d);
+        for (int k = 0; k < NP; ++k) {
+          const float2 te = *reinterpret_cast<const float2*>(iE + r + 2 * k);
+          const float2 to = *reinterpret_cast<const float2*>(iO + r + 2 * k);
+          e[2 * k] = te.x;
+          e[2 * k + 1] = te.y;
+          o[2 * k] = to.x;
+          o[2 * k + 1] = to.y;
+        }
+        f2v A = {0.f, 0.f}, D = {0.f, 0.f};
+#pragma unroll
+        for (int m2 = 0; m2 < H2; ++m2) {
+          const f2v ve = {e[m2], e[m2 + 1]}, vo = {o[m2], o[m2 + 1]};
+          A = __builtin_elementwise_fma((f2v)flo[2 * m2], ve, A);
+          D = __builtin_elementwise_fma((f2v)fhi[2 * m2], ve, D);
+          A = __builtin_elementwise_fma((f2v)flo[2 * m2 + 1], vo, A);
+          D = __builtin_elementwise_fma((f2v)fhi[2 * m2 + 1], vo, D);
         }
         const int i = Sl + r;
-        if (i >= own0 && i < own0 + T) {
-          dout[i] = d;
-          if (last) aout[i] = a;
+        const bool own_a = i >= own0 && i < own0 + T, own_b = i + 1 >= own0 && i + 1 < own0 + T && r + 1 < nl;
+        if (own_a && own_b && dpair) {
+          *reinterpret_cast<float2*>(dout + i) = make_float2(D.x, D.y);
+          if (last) *reinterpret_cast<float2*>(aout + i) = make_float2(A.x, A.y);
+        } else {
+          if (own_a) {
+            dout[i] = D.x;
+            if (last) aout[i] = A.x;
+          }
+          if (own_b) {
+            dout[i + 1] = D.y;
+            if (last) aout[i + 1] = A.y;
+          }
         }
-        if (!last) ((r & 1) ? oO : oE)[r >> 1] = a;
+        if (!last) {
+          oE[r >> 1] = A.x;
+          if (r + 1 < nl) oO[r >> 1] = A.y;
+        }
       }
       __syncthreads();
       iE = oE;
@@ -326,13 +428,17 @@ __device__ __forceinline__ void syn_ranges(const Dwt1Geom& g, int u0, int u1, in
 
 template <int L>
 __global__ void __launch_bounds__(kT1S) k_dwt1_syn(const float* __restrict__ coeffs, float* __restrict__ out,
-                                                 const float* __restrict__ filt, Dwt1Geom g, int nout0, float sc) {
+                                                 const float* __restrict__ filt, Dwt1Geom g, int nout0, float sc,
+                                                 int t_lo, int t_hi) {
   constexpr int p = L - 2;
   constexpr int H2 = L / 2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
-  const int64_t item = blockIdx.x / g.tiles;
-  const int tile = (int)(blockIdx.x % g.tiles);
+  // tiles [t_lo, t_hi) are left to k_dwt1_syn_int; this kernel runs the others (nb per signal)
+  const int nb = g.tiles - (t_hi - t_lo);
+  const int64_t item = blockIdx.x / nb;
+  const int kb = (int)(blockIdx.x % nb);
+  const int tile = kb < t_lo ? kb : t_hi + (kb - t_lo);
   float rlo[L], rhi[L];
 #pragma unroll
   for (int k = 0; k < L; ++k) {
@@ -387,7 +493,150 @@ __global__ void __launch_bounds__(kT1S) k_dwt1_syn(const float* __restrict__ coe
 }
 
 // ------------------------------------------------------------------------------------------------
+// Interior synthesis tiles (no coefficient range clamped at any level): persistent workgroups over
+// (signal, tile) units, shapes fixed at compile time by (L, J). An interior output tile
+// [u0, u0 + 2 kTile0) needs coefficients [u0 >> (l+1), + n_l) of every level l (n_l below) and
+// the same range of A_J-1: about 2 kTile0 floats, fetched into registers one unit ahead (slot
+// counts per band known at compile time, one coalesced load per slot) and stored to LDS in one
+// pass, so the next unit's HBM latency hides behind the current unit's J levels. A thread makes
+// the output pair (2q, 2q + 1), which shares all 2 H2 coefficient reads; the taps keep the order
+// of k_dwt1_syn / k_synthesis_axis (j ascending, lo then hi), so the sums are identical.
+template <int L>
+__host__ __device__ constexpr int syn_n(int l) {  // coefficients of level l for an interior tile
+  int n = 2 * kTile0;
+  for (int i = 0; i <= l; ++i) n = ((n - 1 + L - 2) >> 1) + 1;
+  return n;
+}
+
+template <int L, int J>
+struct SynShape {
+  static constexpr int len(int s) { return syn_n<L>(s < J ? s : J - 1); }  // s = J: A_J-1
+  static constexpr int cum(int s) { return s == 0 ? 0 : cum(s - 1) + ((len(s - 1) + 3) & ~3); }
+  static constexpr int slots(int s) { return (len(s) + kT1 - 1) / kT1; }
+  static constexpr int slot0(int s) { return s == 0 ? 0 : slot0(s - 1) + slots(s - 1); }
+  static constexpr int stage = cum(J + 1);
+  static constexpr int nslots = slot0(J + 1);
+  static constexpr int abuf = (syn_n<L>(0) + 3) & ~3;  // largest reconstructed approximation
+  static constexpr int lds_bytes = 4 * (stage + 2 * abuf);
+};
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+template <int L, int J>
+__global__ void __launch_bounds__(kT1) k_dwt1_syn_int(const float* __restrict__ coeffs, float* __restrict__ out,
+                                                     const float* __restrict__ filt, Dwt1Geom g, int nout0, float sc,
+                                                     int t_lo, int t_hi, int64_t units) {
+  using Sh = SynShape<L, J>;
+  constexpr int H2 = L / 2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  float rlo[L], rhi[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    rlo[k] = filt[k];
+    rhi[k] = filt[L + k];
+  }
+  float* stage = smem;
+  float* abuf0 = smem + Sh::stage;
+  float* abuf1 = abuf0 + Sh::abuf;
+  const int nti = t_hi - t_lo;
+  float pf[Sh::nslots];
+  auto prefetch = [&](int64_t u) {
+    u = u < units ? u : units - 1;
+    const int64_t item = u / nti;
+    const int u0 = (t_lo + (int)(u - item * nti)) * (2 * kTile0);
+    static_for<0, J + 1>([&](auto sv) {
+      constexpr int s = decltype(sv)::value;
+      constexpr int l = s < J ? s : J - 1;
+      constexpr int LEN = Sh::len(s), NS = Sh::slots(s), S0 = Sh::slot0(s);
+      const float* src = coeffs + g.items * (s < J ? g.off_d[l] : g.off_a) + item * (int64_t)g.m[l] + (u0 >> (l + 1));
+      // the last tile's ranges run past the band: clamped (unconditional) loads here, zeros put in
+      // when the unit is staged (k_dwt1_syn's rule)
+      const int vlen = min(LEN, g.m[l] - (u0 >> (l + 1)));
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        const int i = tid + k * kT1;
+        pf[S0 + k] = src[i < vlen ? i : vlen - 1];
+      }
+    });
+  };
+  int64_t u = blockIdx.x;
+  if (u < units) prefetch(u);
+  for (; u < units; u += gridDim.x) {
+    const int64_t item = u / nti;
+    const int u0 = (t_lo + (int)(u - item * nti)) * (2 * kTile0);
+    static_for<0, J + 1>([&](auto sv) {
+      constexpr int s = decltype(sv)::value;
+      constexpr int l = s < J ? s : J - 1;
+      constexpr int LEN = Sh::len(s), NS = Sh::slots(s), S0 = Sh::slot0(s), C = Sh::cum(s);
+      const int vlen = min(LEN, g.m[l] - (u0 >> (l + 1)));
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        const int i = tid + k * kT1;
+        if (i < LEN) stage[C + i] = i < vlen ? sc * pf[S0 + k] : 0.f;
+      }
+    });
+    __syncthreads();
+    prefetch(u + gridDim.x);  // in flight while the levels run
+    float* o = out + item * (int64_t)nout0 + u0;
+    const bool pairs_aligned = (reinterpret_cast<uintptr_t>(o) & 7) == 0;
+    static_for<0, J>([&](auto iv) {
+      constexpr int ll = J - 1 - decltype(iv)::value;  // coarse to fine
+      // coefficient i of level ll sits at i - (u0 >> (ll + 1)); the pair q = outputs (2q, 2q + 1)
+      // relative to the level's first output u0 >> ll reads coefficients q .. q + H2 - 1
+      const float* ain = ll == J - 1 ? stage + Sh::cum(J) : ((ll & 1) ? abuf0 : abuf1);
+      const float* din = stage + Sh::cum(ll);
+      float* aout = (ll & 1) ? abuf1 : abuf0;
+      constexpr int NOUT = ll ? syn_n<L>(ll > 0 ? ll - 1 : 0) : 2 * kTile0;
+      // outputs past the approximation's band (or the signal) are zeros / not written
+      const int vout = ll ? g.m[ll > 0 ? ll - 1 : 0] - (u0 >> ll) : nout0 - u0;
+      for (int q = tid; q < (NOUT + 1) / 2; q += kT1) {
+        float ya = 0.f, yb = 0.f;
+#pragma unroll
+        for (int j = 0; j < H2; ++j) {
+          const float av = ain[q + H2 - 1 - j], dv = din[q + H2 - 1 - j];
+          ya = fmaf(rlo[2 * j], av, ya);
+          ya = fmaf(rhi[2 * j], dv, ya);
+          yb = fmaf(rlo[2 * j + 1], av, yb);
+          yb = fmaf(rhi[2 * j + 1], dv, yb);
+        }
+        if (ll) {
+          aout[2 * q] = 2 * q < vout ? ya : 0.f;
+          if (NOUT % 2 == 0 || 2 * q + 1 < NOUT) aout[2 * q + 1] = 2 * q + 1 < vout ? yb : 0.f;
+        } else if (pairs_aligned && 2 * q + 1 < vout) {
+          *reinterpret_cast<float2*>(o + 2 * q) = make_float2(ya, yb);
+        } else {
+          if (2 * q < vout) o[2 * q] = ya;
+          if (2 * q + 1 < vout) o[2 * q + 1] = yb;
+        }
+      }
+      __syncthreads();
+    });
+  }
+}
+
+
+// ------------------------------------------------------------------------------------------------
 bool mode_ok(int mode) { return mode != WAM_MODE_PERIODIC; }
+
+// the persistent synthesis' register footprint and LDS for (L, J)
+bool syn_int_fits(int L, int J) {
+#define WAM_SF(LL, JJ) \
+  if (L == LL && J == JJ) return SynShape<LL, JJ>::nslots <= 40 && SynShape<LL, JJ>::lds_bytes <= kLds1Cap;
+#define WAM_SFJ(LL) WAM_SF(LL, 1) WAM_SF(LL, 2) WAM_SF(LL, 3) WAM_SF(LL, 4) WAM_SF(LL, 5) WAM_SF(LL, 6) \
+                    WAM_SF(LL, 7) WAM_SF(LL, 8)
+  WAM_SFJ(2) WAM_SFJ(4) WAM_SFJ(6) WAM_SFJ(8) WAM_SFJ(10) WAM_SFJ(12) WAM_SFJ(14) WAM_SFJ(16) WAM_SFJ(18) WAM_SFJ(20)
+#undef WAM_SFJ
+#undef WAM_SF
+  return false;
+}
 
 Dwt1Geom make_geom1(const wam_plan* p, int n, int mode, int64_t items) {
   Dwt1Geom g{};
@@ -513,7 +762,35 @@ int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in,
     }
     WAM_LAUNCH_CHECK();
   }
-  if (nb_blocks > 0) {
+  // boundary tiles: persistent with window prefetch when every boundary window fits kPF * kT1
+  int max_wlen = 0;
+  for (int t = 0; t < g.tiles; ++t) {
+    if (t >= t_lo && t < t_hi) continue;
+    int S[WAM_MAX_LEVELS], E[WAM_MAX_LEVELS], s[WAM_MAX_LEVELS], e[WAM_MAX_LEVELS];
+    ana_ranges(g, t, pp, S, E, s, e);
+    max_wlen = std::max(max_wlen, 2 * (E[0] - S[0]) + pp);
+  }
+  if (nb_blocks > 0 && max_wlen <= kPF * kT1) {
+    int dev = 0;
+    WAM_HIP_CHECK(hipGetDevice(&dev));
+    int cus = 256;
+    WAM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int64_t grid = std::min<int64_t>(nb_blocks, 2LL * cus);
+    WamTimer tm(st, "k_dwt1_ana_p", bytes * (double)(g.tiles - (t_hi - t_lo)) / g.tiles);
+    switch (p->L) {
+#define WAM_D1AP(LL)                                                                                           \
+  case LL:                                                                                                     \
+    if (int rc = lds_opt_in((const void*)k_dwt1_ana_p<LL>, lds)) return rc;                                    \
+    hipLaunchKernelGGL(k_dwt1_ana_p<LL>, dim3((unsigned)grid), dim3(kT1), lds, st, in, coeffs, filt, g, t_lo, t_hi, \
+                       nb_blocks);                                                                             \
+    break;
+      WAM_D1AP(2) WAM_D1AP(4) WAM_D1AP(6) WAM_D1AP(8) WAM_D1AP(10) WAM_D1AP(12) WAM_D1AP(14) WAM_D1AP(16)
+      WAM_D1AP(18) WAM_D1AP(20)
+#undef WAM_D1AP
+      default: return WAM_ERR_UNSUPPORTED;
+    }
+    WAM_LAUNCH_CHECK();
+  } else if (nb_blocks > 0) {
     WamTimer tm(st, "k_dwt1_ana", bytes * (double)(g.tiles - (t_hi - t_lo)) / g.tiles);
     switch (p->L) {
 #define WAM_D1A(LL)                                                                                          \
@@ -543,15 +820,53 @@ int launch_dwt1_tile_synthesis(const wam_plan* p, int64_t batch, const float* co
   if (blocks > 0x7fffffff) return WAM_ERR_UNSUPPORTED;
   const float* filt = p->d_filt + WAM_F_SYN_LO * p->L;
   const int lds = syn_lds_bytes(p);
+  // every tile on the persistent kernel (J <= 8; coefficient ranges are only ever clamped at the
+  // right end, which its zero rule covers), k_dwt1_syn otherwise
+  int t_lo = 0, t_hi = 0;
+  if (g.J <= 8 && syn_int_fits(p->L, g.J)) t_hi = g.tiles;
+  const int64_t units = batch * (int64_t)(t_hi - t_lo);
+  int cus = 256;
+  if (units > 0) {
+    int dev = 0;
+    WAM_HIP_CHECK(hipGetDevice(&dev));
+    WAM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const double bytes_all = 4.0 * ((double)batch * p->band_off[p->nbands] + (double)batch * (double)nout);
+  for (int ai = 0; ai < n_alpha && units > 0; ++ai) {
+    const float sc = alpha ? alpha[ai] : 1.0f;
+    float* o = out + (int64_t)ai * batch * nout;
+    const int64_t grid = std::min<int64_t>(units, 2LL * cus);
+    WamTimer tm(st, "k_dwt1_syn_int", bytes_all * (double)(t_hi - t_lo) / g.tiles);
+    int rc = WAM_ERR_UNSUPPORTED;
+#define WAM_D1SI(LL, JJ)                                                                                        \
+  if (p->L == LL && g.J == JJ) {                                                                                \
+    using Sh = SynShape<LL, JJ>;                                                                                \
+    if (int e = lds_opt_in((const void*)k_dwt1_syn_int<LL, JJ>, Sh::lds_bytes)) return e;                        \
+    hipLaunchKernelGGL((k_dwt1_syn_int<LL, JJ>), dim3((unsigned)grid), dim3(kT1), Sh::lds_bytes, st, coeffs, o, \
+                       filt, g, nout, sc, t_lo, t_hi, units);                                                  \
+    rc = WAM_OK;                                                                                                \
+  }
+#define WAM_D1SJ(LL) WAM_D1SI(LL, 1) WAM_D1SI(LL, 2) WAM_D1SI(LL, 3) WAM_D1SI(LL, 4) WAM_D1SI(LL, 5) \
+                     WAM_D1SI(LL, 6) WAM_D1SI(LL, 7) WAM_D1SI(LL, 8)
+    WAM_D1SJ(2) WAM_D1SJ(4) WAM_D1SJ(6) WAM_D1SJ(8) WAM_D1SJ(10) WAM_D1SJ(12) WAM_D1SJ(14) WAM_D1SJ(16)
+    WAM_D1SJ(18) WAM_D1SJ(20)
+#undef WAM_D1SJ
+#undef WAM_D1SI
+    if (rc) return rc;
+    WAM_LAUNCH_CHECK();
+  }
+  const int64_t nb_blocks = batch * (int64_t)(g.tiles - (t_hi - t_lo));
+  if (nb_blocks == 0) return WAM_OK;
   for (int ai = 0; ai < n_alpha; ++ai) {
     const float sc = alpha ? alpha[ai] : 1.0f;
     float* o = out + (int64_t)ai * batch * nout;
-    WamTimer tm(st, "k_dwt1_syn", 4.0 * ((double)batch * p->band_off[p->nbands] + (double)batch * (double)nout));
+    WamTimer tm(st, "k_dwt1_syn", bytes_all * (double)(g.tiles - (t_hi - t_lo)) / g.tiles);
     switch (p->L) {
 #define WAM_D1S(LL)                                                                                            \
   case LL:                                                                                                     \
     if (int rc = lds_opt_in((const void*)k_dwt1_syn<LL>, lds)) return rc;                                      \
-    hipLaunchKernelGGL(k_dwt1_syn<LL>, dim3((unsigned)blocks), dim3(kT1S), lds, st, coeffs, o, filt, g, nout, sc); \
+    hipLaunchKernelGGL(k_dwt1_syn<LL>, dim3((unsigned)nb_blocks), dim3(kT1S), lds, st, coeffs, o, filt, g, nout, sc, \
+                       t_lo, t_hi);                                                                            \
     break;
       WAM_D1S(2) WAM_D1S(4) WAM_D1S(6) WAM_D1S(8) WAM_D1S(10) WAM_D1S(12) WAM_D1S(14) WAM_D1S(16) WAM_D1S(18)
       WAM_D1S(20)
