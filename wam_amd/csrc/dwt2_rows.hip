@@ -172,11 +172,17 @@ struct MapsArgs {
   int64_t full_items;
 };
 
-template <int L, int C, int VEC, int MAXV>
+// C: channels filtered separately (the per-channel form, numpy's mean-after-DWT order, needed when
+// the caller wants the per-channel coefficient gradients); CIN > 1 (with C == 1): the CIN gradient
+// planes of an image are averaged on the load and ONE plane is filtered (the mean commutes with the
+// linear adjoint -- the k_plane_maps form, equal to fp32 rounding), and the next level's LL is one
+// plane per image. CPL: output columns per lane (strip = 64 CPL columns).
+template <int L, int C, int CIN, int CPL, int VEC, int MAXV>
 __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, int nh, int nw, int64_t in_plane,
                                                   float* __restrict__ ll_out, int mh, int mw,
                                                   const float* __restrict__ filt, int nstrips, int nchunks, int R,
                                                   int64_t total_waves, MapsArgs ma) {
+  static_assert(CIN == 1 || C == 1, "channel mean on load filters one plane");
   constexpr int p = L - 2;
   __shared__ __attribute__((aligned(16))) float rows[kWaves][C][kRowLds];
   const int lane = threadIdx.x & 63;
@@ -194,7 +200,7 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
     flo[k] = filt[k];
     fhi[k] = filt[L + k];
   }
-  const float* src = in + img * C * in_plane;
+  const float* src = in + img * (C * CIN) * in_plane;
   {
     const PadLane pl = pad_lane(lane, nw, p, WAM_MODE_ZERO);
     if (pl.dst >= 0) {
@@ -202,42 +208,64 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
       for (int c = 0; c < C; ++c) rows[wv][c][pl.dst] = 0.f;
     }
   }
-  const int j = strip * 64 + lane;
-  const bool jv = j < mw;
-  const int jc = jv ? j : mw - 1;
+  int jcol[CPL];
+  bool jv[CPL];
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    const int j = strip * 64 * CPL + lane + 64 * q;
+    jv[q] = j < mw;
+    jcol[q] = j;
+  }
   const int i0 = chunk * R;
   const int i1 = min(mh, i0 + R);
   const int er0 = 2 * i0 - p;
   const int64_t out_plane = (int64_t)mh * mw;
 
-  RowRegs<VEC, MAXV> f[2][C];
-  auto fetch = [&](RowRegs<VEC, MAXV> (&r)[C], int er) {
+  constexpr int NF = C * CIN;  // source rows fetched per extended row
+  RowRegs<VEC, MAXV> f[2][NF];
+  auto fetch = [&](RowRegs<VEC, MAXV> (&r)[NF], int er) {
     const bool valid = er >= 0 && er < nh;  // zero padding
     const int rr = valid ? er : 0;
 #pragma unroll
-    for (int c = 0; c < C; ++c) r[c].fetch(src + c * in_plane + (int64_t)rr * nw, nw, lane, valid);
+    for (int c = 0; c < NF; ++c) r[c].fetch(src + c * in_plane + (int64_t)rr * nw, nw, lane, valid);
   };
-  auto process = [&](const RowRegs<VEC, MAXV> (&r)[C], float (&lo)[C], float (&hi)[C]) {
+  auto process = [&](RowRegs<VEC, MAXV> (&r)[NF], float (&lo)[C][CPL], float (&hi)[C][CPL]) {
+    if constexpr (CIN > 1) {  // ((g0 + g1) + g2) * (1 / CIN), as k_plane_maps averages on its load
+      constexpr float inv = 1.0f / (float)CIN;
 #pragma unroll
-    for (int c = 0; c < C; ++c) r[c].commit(rows[wv][c], lane, nullptr);
+      for (int i = 0; i < VEC * MAXV; ++i) {
+        float sum = r[0].v[i];
+#pragma unroll
+        for (int c = 1; c < CIN; ++c) sum += r[c].v[i];
+        r[0].v[i] = sum * inv;
+      }
+      r[0].commit(rows[wv][0], lane, nullptr);
+    } else {
+#pragma unroll
+      for (int c = 0; c < C; ++c) r[c].commit(rows[wv][c], lane, nullptr);
+    }
     wsync();
 #pragma unroll
-    for (int c = 0; c < C; ++c) hfilter<L>(rows[wv][c], jc, p, flo, fhi, lo[c], hi[c]);
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) hfilter<L>(rows[wv][c], jv[q] ? jcol[q] : mw - 1, p, flo, fhi, lo[c][q], hi[c][q]);
     wsync();
   };
 
-  float rl[C][L], rh[C][L];
+  float rl[C][CPL][L], rh[C][CPL][L];
   fetch(f[0], er0);
 #pragma unroll
   for (int k = 0; k < L - 2; ++k) {
     fetch(f[(k + 1) & 1], er0 + k + 1);
-    float lo[C], hi[C];
+    float lo[C][CPL], hi[C][CPL];
     process(f[k & 1], lo, hi);
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      rl[c][k] = lo[c];
-      rh[c][k] = hi[c];
-    }
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) {
+        rl[c][q][k] = lo[c][q];
+        rh[c][q][k] = hi[c][q];
+      }
   }
   float mx_h = 0.f, mx_v = 0.f, mx_d = 0.f, mx_a = 0.f;
   const bool last = ma.off_a >= 0;
@@ -245,65 +273,72 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
   for (int i = i0; i < i1; ++i) {
     const int er = er0 + 2 * (i - i0) + L - 2;
     fetch(f[1], er + 1);
-    float lo[C], hi[C];
+    float lo[C][CPL], hi[C][CPL];
     process(f[0], lo, hi);
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      rl[c][L - 2] = lo[c];
-      rh[c][L - 2] = hi[c];
-    }
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) {
+        rl[c][q][L - 2] = lo[c][q];
+        rh[c][q][L - 2] = hi[c][q];
+      }
     fetch(f[0], er + 2);
     process(f[1], lo, hi);
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      rl[c][L - 1] = lo[c];
-      rh[c][L - 1] = hi[c];
-    }
-    float sa = 0.f, sh = 0.f, sv = 0.f, sd = 0.f;
-    const int64_t o = (int64_t)i * mw + j;
+    for (int c = 0; c < C; ++c)
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      float a = 0.f, h = 0.f, v = 0.f, d = 0.f;
-#pragma unroll
-      for (int k = 0; k < L; ++k) {
-        a = fmaf(flo[k], rl[c][k], a);
-        h = fmaf(fhi[k], rl[c][k], h);
-        v = fmaf(flo[k], rh[c][k], v);
-        d = fmaf(fhi[k], rh[c][k], d);
+      for (int q = 0; q < CPL; ++q) {
+        rl[c][q][L - 1] = lo[c][q];
+        rh[c][q][L - 1] = hi[c][q];
       }
-      if (jv) {
-        const int64_t plane = img * C + c;
-        if (!last) ll_out[plane * out_plane + o] = a;
-        if (ma.full) {  // band-major: band b starts at full_items * off_b
-          ma.full[ma.full_items * ma.off_h + plane * out_plane + o] = h;
-          ma.full[ma.full_items * ma.off_v + plane * out_plane + o] = v;
-          ma.full[ma.full_items * ma.off_d + plane * out_plane + o] = d;
-          if (last) ma.full[ma.full_items * ma.off_a + plane * out_plane + o] = a;
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      float sa = 0.f, sh = 0.f, sv = 0.f, sd = 0.f;
+      const int64_t o = (int64_t)i * mw + jcol[q];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        float a = 0.f, h = 0.f, v = 0.f, d = 0.f;
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+          a = fmaf(flo[k], rl[c][q][k], a);
+          h = fmaf(fhi[k], rl[c][q][k], h);
+          v = fmaf(flo[k], rh[c][q][k], v);
+          d = fmaf(fhi[k], rh[c][q][k], d);
+        }
+        if (jv[q]) {
+          const int64_t plane = img * C + c;
+          if (!last) ll_out[plane * out_plane + o] = a;
+          if (ma.full) {  // band-major: band b starts at full_items * off_b
+            ma.full[ma.full_items * ma.off_h + plane * out_plane + o] = h;
+            ma.full[ma.full_items * ma.off_v + plane * out_plane + o] = v;
+            ma.full[ma.full_items * ma.off_d + plane * out_plane + o] = d;
+            if (last) ma.full[ma.full_items * ma.off_a + plane * out_plane + o] = a;
+          }
+        }
+        // numpy float32 mean over the channel axis: sequential sum, then true_divide
+        sa = c == 0 ? a : sa + a;
+        sh = c == 0 ? h : sh + h;
+        sv = c == 0 ? v : sv + v;
+        sd = c == 0 ? d : sd + d;
+#pragma unroll
+        for (int k = 0; k < L - 2; ++k) {
+          rl[c][q][k] = rl[c][q][k + 2];
+          rh[c][q][k] = rh[c][q][k + 2];
         }
       }
-      // numpy float32 mean over the channel axis: sequential sum, then true_divide
-      sa = c == 0 ? a : sa + a;
-      sh = c == 0 ? h : sh + h;
-      sv = c == 0 ? v : sv + v;
-      sd = c == 0 ? d : sd + d;
-#pragma unroll
-      for (int k = 0; k < L - 2; ++k) {
-        rl[c][k] = rl[c][k + 2];
-        rh[c][k] = rh[c][k + 2];
-      }
-    }
-    if (jv) {
-      const float mh_ = fabsf(sh / (float)C), mv_ = fabsf(sv / (float)C), md_ = fabsf(sd / (float)C);
-      mrow[ma.off_h + o] = mh_;
-      mrow[ma.off_v + o] = mv_;
-      mrow[ma.off_d + o] = md_;
-      mx_h = nan_max(mx_h, mh_);
-      mx_v = nan_max(mx_v, mv_);
-      mx_d = nan_max(mx_d, md_);
-      if (last) {
-        const float ma_ = fabsf(sa / (float)C);
-        mrow[ma.off_a + o] = ma_;
-        mx_a = nan_max(mx_a, ma_);
+      if (jv[q]) {
+        const float mh_ = fabsf(sh / (float)C), mv_ = fabsf(sv / (float)C), md_ = fabsf(sd / (float)C);
+        mrow[ma.off_h + o] = mh_;
+        mrow[ma.off_v + o] = mv_;
+        mrow[ma.off_d + o] = md_;
+        mx_h = nan_max(mx_h, mh_);
+        mx_v = nan_max(mx_v, mv_);
+        mx_d = nan_max(mx_d, md_);
+        if (last) {
+          const float ma_ = fabsf(sa / (float)C);
+          mrow[ma.off_a + o] = ma_;
+          mx_a = nan_max(mx_a, ma_);
+        }
       }
     }
   }
@@ -378,39 +413,53 @@ int dispatch_ana(int64_t batch, const float* in, int nh, int nw, int mh, int mw,
   return dispatch_ana_cpl<L, 1>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
 }
 
-template <int L, int C, int VEC, int MAXV>
+template <int L, int C, int CIN, int CPL, int VEC, int MAXV>
 int launch_adj_t(int64_t images, const float* in, int nh, int nw, int mh, int mw, const float* filt, float* ll_out,
                  const MapsArgs& ma, hipStream_t st) {
-  const int nstrips = (mw + 63) / 64;
+  const int nstrips = (mw + 64 * CPL - 1) / (64 * CPL);
   int nchunks, R;
   pick_chunks(images * nstrips, mh, nchunks, R);
   const int64_t waves = images * nstrips * nchunks;
   const bool last = ma.off_a >= 0;
-  double bytes = 4.0 * (double)images * ((double)C * nh * nw + 4.0 * mh * mw + (last ? 0.0 : (double)C * mh * mw) +
+  double bytes = 4.0 * (double)images * ((double)C * CIN * nh * nw + 4.0 * mh * mw + (last ? 0.0 : (double)C * mh * mw) +
                                          (ma.full ? (double)C * 4 * mh * mw : 0.0));
   WamTimer tm(st, "k_adj_maps", bytes);
-  hipLaunchKernelGGL((k_adj_maps<L, C, VEC, MAXV>), dim3((unsigned)((waves + kWaves - 1) / kWaves)), dim3(256), 0, st,
-                     in, nh, nw, (int64_t)nh * nw, ll_out, mh, mw, filt, nstrips, nchunks, R, waves, ma);
+  hipLaunchKernelGGL((k_adj_maps<L, C, CIN, CPL, VEC, MAXV>), dim3((unsigned)((waves + kWaves - 1) / kWaves)),
+                     dim3(256), 0, st, in, nh, nw, (int64_t)nh * nw, ll_out, mh, mw, filt, nstrips, nchunks, R, waves,
+                     ma);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }
 
-template <int L, int C>
+template <int L, int C, int CIN, int CPL>
 int dispatch_adj_c(int64_t images, const float* in, int nh, int nw, int mh, int mw, const float* filt, float* ll_out,
                    const MapsArgs& ma, hipStream_t st) {
   const bool vec4 = (nw % 4 == 0) && ((uintptr_t)in % 16 == 0);
   if (vec4)
-    return nw <= 256 ? launch_adj_t<L, C, 4, 1>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st)
-                     : launch_adj_t<L, C, 4, 2>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
-  return nw <= 128 ? launch_adj_t<L, C, 1, 2>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st)
-                   : launch_adj_t<L, C, 1, 8>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    return nw <= 256 ? launch_adj_t<L, C, CIN, CPL, 4, 1>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st)
+                     : launch_adj_t<L, C, CIN, CPL, 4, 2>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+  return nw <= 128 ? launch_adj_t<L, C, CIN, CPL, 1, 2>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st)
+                   : launch_adj_t<L, C, CIN, CPL, 1, 8>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
 }
 
+// mean_first: the channel mean on the load (one plane filtered; LL out one plane per image)
 template <int L>
-int dispatch_adj(int channels, int64_t images, const float* in, int nh, int nw, int mh, int mw, const float* filt,
-                 float* ll_out, const MapsArgs& ma, hipStream_t st) {
-  if (channels == 3) return dispatch_adj_c<L, 3>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
-  if (channels == 1) return dispatch_adj_c<L, 1>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+int dispatch_adj(int channels, bool mean_first, int64_t images, const float* in, int nh, int nw, int mh, int mw,
+                 const float* filt, float* ll_out, const MapsArgs& ma, hipStream_t st) {
+  // up to three output columns per lane: fewer strips (each strip refetches and recommits whole rows)
+  // (three spill the register rings past 12 taps)
+  const int cpl = mw <= 64 ? 1 : (mw <= 128 || L > 12 ? 2 : 3);
+  if (channels == 3 && mean_first) {
+    if (cpl == 1) return dispatch_adj_c<L, 1, 3, 1>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    if (cpl == 2) return dispatch_adj_c<L, 1, 3, 2>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    return dispatch_adj_c<L, 1, 3, 3>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+  }
+  if (channels == 3) return dispatch_adj_c<L, 3, 1, 1>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+  if (channels == 1) {
+    if (cpl == 1) return dispatch_adj_c<L, 1, 1, 1>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    if (cpl == 2) return dispatch_adj_c<L, 1, 1, 2>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    return dispatch_adj_c<L, 1, 1, 3>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+  }
   return WAM_ERR_UNSUPPORTED;
 }
 
@@ -442,9 +491,10 @@ int launch_dwt2_analysis_rows(const wam_plan* p, int64_t batch, const float* in,
   }
 }
 
-int launch_dwt2_adjoint_maps_level(const wam_plan* p, int level, int64_t images, int channels, int64_t group_items,
-                                   const float* in, const int64_t* in_dims, float* ll_out, float* maps,
-                                   float* band_max, float* full_grads, int64_t full_items, hipStream_t st) {
+int launch_dwt2_adjoint_maps_level(const wam_plan* p, int level, int64_t images, int channels, bool mean_first,
+                                   int64_t group_items, const float* in, const int64_t* in_dims, float* ll_out,
+                                   float* maps, float* band_max, float* full_grads, int64_t full_items, hipStream_t st) {
+  if (mean_first && full_grads) return WAM_ERR_INVALID_ARG;  // per-channel grads need the per-channel form
   const float* filt = p->d_filt + WAM_F_ADJ_LO * p->L;
   const int nh = (int)in_dims[0], nw = (int)in_dims[1];
   const int mh = (int)p->lout[level][0], mw = (int)p->lout[level][1];
@@ -465,13 +515,13 @@ int launch_dwt2_adjoint_maps_level(const wam_plan* p, int level, int64_t images,
   ma.group_items = group_items;
   ma.full_items = full_items;
   switch (p->L) {
-    case 2: return dispatch_adj<2>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
-    case 4: return dispatch_adj<4>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
-    case 6: return dispatch_adj<6>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
-    case 8: return dispatch_adj<8>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
-    case 12: return dispatch_adj<12>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
-    case 16: return dispatch_adj<16>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
-    case 20: return dispatch_adj<20>(channels, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    case 2: return dispatch_adj<2>(channels, mean_first, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    case 4: return dispatch_adj<4>(channels, mean_first, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    case 6: return dispatch_adj<6>(channels, mean_first, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    case 8: return dispatch_adj<8>(channels, mean_first, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    case 12: return dispatch_adj<12>(channels, mean_first, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    case 16: return dispatch_adj<16>(channels, mean_first, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
+    case 20: return dispatch_adj<20>(channels, mean_first, images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
     default: return WAM_ERR_UNSUPPORTED;
   }
 }

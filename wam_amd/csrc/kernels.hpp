@@ -24,9 +24,11 @@ bool dwt2_rows_supported(const wam_plan* p, int level, bool adjoint);
 int launch_dwt2_analysis_rows(const wam_plan* p, int64_t batch, const float* in, const int64_t* in_dims,
                               const int64_t* out_dims, int mode, int fset, float* out_a, float* const* sub,
                               const struct WamNoise* noise, hipStream_t st);
-int launch_dwt2_adjoint_maps_level(const wam_plan* p, int level, int64_t images, int channels, int64_t group_items,
-                                   const float* in, const int64_t* in_dims, float* ll_out, float* maps,
-                                   float* band_max, float* full_grads, int64_t full_items, hipStream_t st);
+// mean_first: the C gradient planes of an image averaged on the load, one plane filtered (level 0
+// of the maps-only pass; LL out is then one plane per image and later levels take channels = 1)
+int launch_dwt2_adjoint_maps_level(const wam_plan* p, int level, int64_t images, int channels, bool mean_first,
+                                   int64_t group_items, const float* in, const int64_t* in_dims, float* ll_out,
+                                   float* maps, float* band_max, float* full_grads, int64_t full_items, hipStream_t st);
 
 // fused SmoothGrad noise on the analysis load (Philox4x32-10, same stream as wam_noise_add)
 struct WamNoise {

@@ -451,19 +451,24 @@ int wam_waverec_adjoint_maps(const wam_plan* p, int64_t groups, int64_t group_it
       return analysis_driver(p, planes, grad, coeff_grads, ws, st, true);
     }
   }
+  // per level (rows kernels): maps from the channel mean taken on the level-0 load (the plane
+  // kernels' form: one plane filtered per image at every level); the per-channel coefficient
+  // gradients, when asked for, by a separate adjoint afterwards
   float* w = (float*)ws;
-  int64_t ll = planes * wam_prod(p->lout[0], 2);
+  int64_t ll = images * wam_prod(p->lout[0], 2);
   float* llbuf[2] = {w, w + ll};
   const float* cur = grad;
   for (int l = 0; l < p->levels; ++l) {
     int64_t in_dims[2];
     for (int a = 0; a < 2; ++a) in_dims[a] = (l == 0) ? p->rec_shape[a] : p->lin[l][a];
     float* ll_out = (l == p->levels - 1) ? nullptr : llbuf[l & 1];
-    int rc = launch_dwt2_adjoint_maps_level(p, l, images, channels, group_items, cur, in_dims, ll_out, maps, band_max,
-                                            coeff_grads, planes, st);
+    const bool mean_first = l == 0 && channels > 1;
+    int rc = launch_dwt2_adjoint_maps_level(p, l, images, l == 0 ? channels : 1, mean_first, group_items, cur, in_dims,
+                                            ll_out, maps, band_max, nullptr, images, st);
     if (rc) return rc;
     cur = ll_out;
   }
+  if (coeff_grads) return analysis_driver(p, planes, grad, coeff_grads, ws, st, true);
   return WAM_OK;
 }
 
