@@ -181,6 +181,14 @@ int wam_frame_accumulate(int64_t groups, int64_t group_items, int64_t frame_len,
                          const float* band_max, int n_bands, int normalize, double* frame,
                          void* stream);
 
+/* wam_frame_accumulate in coefficient order (same sums, bit-identical): dst[k] = the frame pixel
+ * of packed coefficient k or -1, cband[k] its band (the inverse of the injective src/band mosaic
+ * map, built by the caller: wam_amd/plan.py frame_accumulate). The maps are read as contiguous
+ * rows, only the fp64 frame goes through the mosaic. */
+int wam_frame_accumulate_coef(int64_t groups, int64_t group_items, int64_t maps_item_len, int64_t frame_len,
+                              const int32_t* dst, const int32_t* cband, const float* maps,
+                              const float* band_max, int n_bands, int normalize, double* frame, void* stream);
+
 /* Integrated-Gradients mosaic + trapezoid (np.trapz(np.nan_to_num(G), axis=1), dx = 1, fp32).
  * For step k = k0 + s, s in [0, groups):  G = nan_to_num(fp32 mosaic value (normalised));
  *   sequential (weights == NULL): if k > 0: acc += (prev + G) / 2;  prev = G

@@ -204,6 +204,48 @@ __global__ void __launch_bounds__(256) k_frame_accumulate(int64_t groups, int64_
   }
 }
 
+// the same accumulation in COEFFICIENT order (dst = frame pixel of coefficient k or -1; the mosaic
+// is injective): the maps are read as contiguous rows (whole cache lines) and only the fp64 frame
+// is addressed through the mosaic, so the partial lines at band-row edges fall on the 16-B/pixel
+// frame instead of the per-sample map reads. Per pixel the sum order is unchanged (bit-identical).
+__global__ void __launch_bounds__(256) k_frame_accumulate_coef(int64_t groups, int64_t group_items,
+                                                               int64_t maps_item_len, int64_t frame_len,
+                                                               const int32_t* __restrict__ dst,
+                                                               const int32_t* __restrict__ cband,
+                                                               const float* __restrict__ maps,
+                                                               const float* __restrict__ band_max, int n_bands,
+                                                               int normalize, double* __restrict__ frame) {
+  const int64_t total = group_items * maps_item_len;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = t / maps_item_len;
+    const int64_t k = t - n * maps_item_len;
+    const int32_t d = dst[k];
+    if (d < 0) continue;
+    const int32_t b = cband[k];
+    double* fp = frame + n * frame_len + d;
+    double acc = *fp;
+    const float* mp = maps + t;
+    const int64_t mstride = group_items * maps_item_len;
+    int64_t s = 0;
+    for (; s + 8 <= groups; s += 8) {
+      float v[8], m[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[u] = mp[(s + u) * mstride];
+        m[u] = normalize ? band_max[(s + u) * n_bands + b] : 1.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += (double)(normalize ? v[u] / m[u] : v[u]);
+    }
+    for (; s < groups; ++s) {
+      float v = mp[s * mstride];
+      if (normalize) v = v / band_max[s * n_bands + b];
+      acc += (double)v;
+    }
+    *fp = acc;
+  }
+}
+
 __device__ __forceinline__ float nan_to_num(float v) {
   if (v != v) return 0.f;
   if (isinf(v)) return v > 0 ? 3.4028234663852886e+38f : -3.4028234663852886e+38f;
@@ -528,6 +570,22 @@ int wam_frame_accumulate(int64_t groups, int64_t group_items, int64_t frame_len,
               4.0 * (double)groups * group_items * frame_len + 16.0 * group_items * frame_len + 8.0 * frame_len);
   hipLaunchKernelGGL(k_frame_accumulate, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, groups,
                      group_items, frame_len, src, band, maps, maps_item_len, band_max, n_bands, normalize, frame);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int wam_frame_accumulate_coef(int64_t groups, int64_t group_items, int64_t maps_item_len, int64_t frame_len,
+                              const int32_t* dst, const int32_t* cband, const float* maps, const float* band_max,
+                              int n_bands, int normalize, double* frame, void* stream) {
+  if (groups < 0 || group_items < 0 || maps_item_len < 0 || frame_len < 0 || !dst || !cband || !maps || !frame)
+    return WAM_ERR_INVALID_ARG;
+  if (normalize && !band_max) return WAM_ERR_INVALID_ARG;
+  const int64_t work = group_items * maps_item_len;
+  if (work == 0 || groups == 0) return WAM_OK;
+  WamTimer tm((hipStream_t)stream, "k_frame_accumulate_coef",
+              4.0 * (double)groups * group_items * frame_len + 16.0 * group_items * frame_len + 8.0 * frame_len);
+  hipLaunchKernelGGL(k_frame_accumulate_coef, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, groups,
+                     group_items, maps_item_len, frame_len, dst, cband, maps, band_max, n_bands, normalize, frame);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }

@@ -232,8 +232,37 @@ def subband_maps(plan, coeff_grads, groups, group_items, channels, maps=None, ba
     return maps, band_max
 
 
+_INV = {}
+
+
+def _inverse_map(gmap, maps_item_len):
+    """(dst, cband) per packed coefficient from the per-pixel (src, band) mosaic map, or None when
+    the map is not injective (cached per map)."""
+    src, band = gmap
+    key = (src.data_ptr(), band.data_ptr(), int(maps_item_len))
+    if key not in _INV:
+        valid = src >= 0
+        pix = torch.nonzero(valid).reshape(-1)
+        s = src[valid].long()
+        dst = torch.full((maps_item_len,), -1, dtype=torch.int32, device=src.device)
+        cband = torch.zeros((maps_item_len,), dtype=torch.int32, device=src.device)
+        ok = s.numel() == 0 or (int(s.max()) < maps_item_len and torch.unique(s).numel() == s.numel())
+        if ok:
+            dst[s] = pix.to(torch.int32)
+            cband[s] = band[valid]
+        _INV[key] = (dst, cband, gmap) if ok else None  # gmap kept alive: its pointers are the key
+    v = _INV[key]
+    return None if v is None else v[:2]
+
+
 def frame_accumulate(groups, group_items, gmap, maps, maps_item_len, band_max, n_bands, normalize, frame):
     src, band = gmap
+    inv = _inverse_map(gmap, maps_item_len)
+    if inv is not None:  # coefficient order: contiguous map reads
+        check(lib.wam_frame_accumulate_coef(groups, group_items, maps_item_len, src.numel(), ptr(inv[0]), ptr(inv[1]),
+                                            ptr(maps), ptr(band_max), n_bands, int(bool(normalize)), ptr(frame),
+                                            stream_of(frame.device)))
+        return
     check(lib.wam_frame_accumulate(groups, group_items, src.numel(), ptr(src), ptr(band), ptr(maps),
                                    maps_item_len, ptr(band_max), n_bands, int(bool(normalize)), ptr(frame),
                                    stream_of(frame.device)))
