@@ -41,10 +41,12 @@ __global__ void __launch_bounds__(256) k_dwt2_ana(const float* __restrict__ in, 
   const int wv = threadIdx.x >> 6;
   const int64_t gw = (int64_t)blockIdx.x * 4 + wv;
   if (gw >= total_waves) return;
-  const int chunk = (int)(gw % nchunks);
-  const int64_t t = gw / nchunks;
-  const int strip = (int)(t % nstrips);
-  const int64_t plane = t / nstrips;
+  // strip fastest: the strips of one (plane, row chunk) -- which fetch the same source rows --
+  // are waves of one workgroup (one CU, one XCD L2) instead of landing on different XCDs
+  const int strip = (int)(gw % nstrips);
+  const int64_t t = gw / nstrips;
+  const int chunk = (int)(t % nchunks);
+  const int64_t plane = t / nchunks;
 
   float flo[L], fhi[L];
 #pragma unroll
@@ -134,10 +136,12 @@ __global__ void __launch_bounds__(256) k_dwt2_syn(const float* __restrict__ A, c
   const int wv = threadIdx.x >> 6;
   const int64_t gw = (int64_t)blockIdx.x * 4 + wv;
   if (gw >= total_waves) return;
-  const int chunk = (int)(gw % nchunks);
-  const int64_t t = gw / nchunks;
-  const int strip = (int)(t % nstrips);
-  const int64_t plane = t / nstrips;
+  // strip fastest: the strips of one (plane, row chunk) -- which fetch the same source rows --
+  // are waves of one workgroup (one CU, one XCD L2) instead of landing on different XCDs
+  const int strip = (int)(gw % nstrips);
+  const int64_t t = gw / nstrips;
+  const int chunk = (int)(t % nchunks);
+  const int64_t plane = t / nchunks;
 
   float rlo[L], rhi[L];
 #pragma unroll
