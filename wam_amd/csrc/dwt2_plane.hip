@@ -174,12 +174,19 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
       for (int c = 0; c < NCH; ++c) fr[c].fetch(src + c * in_plane + (int64_t)(valid ? sr : 0) * nw, nw, lane, valid);
     };
-    // horizontal pass of ext row e into its ring slot
-    auto hrow = [&](RowRegs<4, 1> (&fr)[NCH], int sr, int e) {
-      float nzr[4];
-      if constexpr (NOISE)
-        make_noise<1>(nzr, nw, lane, (ch * nh + (sr >= 0 ? sr : 0)) * (int64_t)nw, sg, img + nz.image_base, smp,
-                      nz.k0, nz.k1, sr >= 0);
+    // SmoothGrad noise of the two ext rows a wave owns in a block, generated together (two
+    // interleaved Philox chains). Element group g = (row's first element) / 4 + lane < 2^32 (host
+    // check), so wam_normal4_x2 reproduces wam_normal4's stream; lanes past the row are never stored.
+    auto noise2 = [&](float (&za)[4], float (&zb)[4], int sra, int srb) {
+      if constexpr (NOISE) {
+        const uint32_t rowg = (uint32_t)(ch * nh) * (uint32_t)nw / 4u + (uint32_t)lane;
+        const uint32_t nw4 = (uint32_t)nw / 4u;
+        wam_normal4_x2(rowg + (uint32_t)(sra >= 0 ? sra : 0) * nw4, rowg + (uint32_t)(srb >= 0 ? srb : 0) * nw4,
+                       (uint32_t)(img + nz.image_base), (uint32_t)smp, nz.k0, nz.k1, za, zb);
+      }
+    };
+    // horizontal pass of ext row e into its ring slot (nzr: its noise, from noise2)
+    auto hrow = [&](RowRegs<4, 1> (&fr)[NCH], int sr, int e, const float (&nzr)[4]) {
       float4 o = fr[0].ok[0] ? make_float4(fr[0].v[0], fr[0].v[1], fr[0].v[2], fr[0].v[3])
                              : make_float4(0.f, 0.f, 0.f, 0.f);
       if constexpr (NCH > 1) {
@@ -198,10 +205,12 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
         if (!fr[0].ok[0]) o = make_float4(0.f, 0.f, 0.f, 0.f);
       }
       if constexpr (NOISE) {
-        o.x = fmaf(sg, nzr[0], o.x);
-        o.y = fmaf(sg, nzr[1], o.y);
-        o.z = fmaf(sg, nzr[2], o.z);
-        o.w = fmaf(sg, nzr[3], o.w);
+        // zero rows (sr < 0, wave-uniform) stay zero: fma(0, z, 0) with a finite z
+        const float sgr = sr >= 0 ? sg : 0.f;
+        o.x = fmaf(sgr, nzr[0], o.x);
+        o.y = fmaf(sgr, nzr[1], o.y);
+        o.z = fmaf(sgr, nzr[2], o.z);
+        o.w = fmaf(sgr, nzr[3], o.w);
       }
       if (lane * 4 < nw) *reinterpret_cast<float4*>(wrow + PADL + lane * 4) = o;
       wsync();
@@ -283,14 +292,20 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
       fetch(F[u][0], S[u][0], 16 * u + 2 * wv);
       fetch(F[u][1], S[u][1], 16 * u + 2 * wv + 1);
     }
-    if (wv < p) hrow(fp, spro, wv - p);
+    if (wv < p) {
+      float za[4] = {0.f, 0.f, 0.f, 0.f}, zb[4];
+      noise2(za, zb, spro, spro);
+      hrow(fp, spro, wv - p, za);
+    }
     for (int b0 = 0; b0 < nb; b0 += D) {
 #pragma unroll
       for (int u = 0; u < D; ++u) {
         const int b = b0 + u;
         if (b < nb) {  // workgroup-uniform
-          hrow(F[u][0], S[u][0], 16 * b + 2 * wv);
-          hrow(F[u][1], S[u][1], 16 * b + 2 * wv + 1);
+          float za[4] = {0.f, 0.f, 0.f, 0.f}, zb[4] = {0.f, 0.f, 0.f, 0.f};
+          noise2(za, zb, S[u][0], S[u][1]);
+          hrow(F[u][0], S[u][0], 16 * b + 2 * wv, za);
+          hrow(F[u][1], S[u][1], 16 * b + 2 * wv + 1, zb);
         }
         // refill: block b + D (past the plane: clamped rows, never consumed)
         fetch(F[u][0], S[u][0], 16 * (b + D) + 2 * wv);
@@ -887,6 +902,8 @@ int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in
   const double bytes = 4.0 * (in_planes * nh0 * nw0 + (double)items * p->band_off[p->nbands]);
   if (nz) {
     if (items != n_samples * nz->images * nz->channels) return WAM_ERR_INVALID_ARG;
+    // the fused noise counts element groups of an image in 32 bits (wam_normal4_x2)
+    if ((int64_t)nz->channels * nh0 * nw0 >= (int64_t(1) << 34)) return WAM_ERR_UNSUPPORTED;
     return dispatch_plane<true, 0, false>(p, g, lds_bytes, items, in, coeffs, nullptr, filt, *nz, n_samples, 1,
                                           "k_plane_ana<noise>", bytes, st);
   }

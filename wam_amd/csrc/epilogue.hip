@@ -481,11 +481,24 @@ __global__ void __launch_bounds__(256) k_disentangle(int64_t items, int size, in
 }
 
 
-// Streaming copy (16-B loads / stores, grid-stride): the measured HBM ceiling bench.py reports
-// beside the 8 TB/s spec peak.
-__global__ void __launch_bounds__(256) k_copy(int64_t n4, const float4* __restrict__ src, float4* __restrict__ dst) {
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n4; t += (int64_t)gridDim.x * blockDim.x)
-    dst[t] = src[t];
+// Streaming copy: the measured HBM ceiling bench.py reports beside the 8 TB/s spec peak. Each
+// thread keeps kCopyU 16-B loads in flight (all issued before the first store) and walks the
+// buffer in grid-sized strides of kCopyU * blockDim float4 per block; nontemporal loads / stores
+// (streamed once, no reuse).
+constexpr int kCopyU = 4;
+typedef float wam_f4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) k_copy(int64_t n4, const wam_f4* __restrict__ src, wam_f4* __restrict__ dst) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x * kCopyU;
+  int64_t t = (int64_t)blockIdx.x * blockDim.x * kCopyU + threadIdx.x;
+  for (; t + (kCopyU - 1) * (int64_t)blockDim.x < n4; t += step) {
+    wam_f4 v[kCopyU];
+#pragma unroll
+    for (int u = 0; u < kCopyU; ++u) v[u] = __builtin_nontemporal_load(src + t + u * (int64_t)blockDim.x);
+#pragma unroll
+    for (int u = 0; u < kCopyU; ++u) __builtin_nontemporal_store(v[u], dst + t + u * (int64_t)blockDim.x);
+  }
+  for (int u = 0; u < kCopyU; ++u, t += blockDim.x)  // the tail (< kCopyU * blockDim per block)
+    if (t < n4) dst[t] = src[t];
 }
 
 }  // namespace
@@ -684,8 +697,9 @@ int wam_copy(int64_t bytes, const void* src, void* dst, void* stream) {
   const int64_t n4 = bytes / 16;
   if (n4 == 0) return WAM_OK;
   WamTimer tm((hipStream_t)stream, "k_copy", 2.0 * bytes);
-  hipLaunchKernelGGL(k_copy, dim3(wam_grid(n4, 256, 256 * 64)), dim3(256), 0, (hipStream_t)stream, n4,
-                     (const float4*)src, (float4*)dst);
+  hipLaunchKernelGGL(k_copy, dim3(wam_grid((n4 + kCopyU - 1) / kCopyU, 256, 256 * 32)), dim3(256), 0,
+                     (hipStream_t)stream, n4,
+                     (const wam_f4*)src, (wam_f4*)dst);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }
