@@ -141,6 +141,19 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
   float* bufA = smem;
   float* bufB = smem + g.llcap;
 
+  // SmoothGrad noise of two source rows sra, srb (< 0: zero rows, any value) of this plane,
+  // generated together (two interleaved Philox chains). Element group g = (row's first element) / 4
+  // + lane < 2^32 (host check), so wam_normal4_x2 reproduces wam_normal4's stream; lanes past the
+  // row are never stored.
+  auto noise2 = [&](float (&za)[4], float (&zb)[4], int sra, int srb) {
+    if constexpr (NOISE) {
+      const uint32_t rowg = (uint32_t)(ch * nh) * (uint32_t)nw / 4u + (uint32_t)lane;
+      const uint32_t nw4 = (uint32_t)nw / 4u;
+      wam_normal4_x2(rowg + (uint32_t)(sra >= 0 ? sra : 0) * nw4, rowg + (uint32_t)(srb >= 0 ? srb : 0) * nw4,
+                     (uint32_t)(img + nz.image_base), (uint32_t)smp, nz.k0, nz.k1, za, zb);
+    }
+  };
+
   // ================================================================ phase 1: level 1 (finest)
   if constexpr (COOP) {
     // Cooperative row stream. Extended rows e (ext row e = source row wam_ext_index(e)) are
@@ -173,17 +186,6 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
       sr_out = sr;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) fr[c].fetch(src + c * in_plane + (int64_t)(valid ? sr : 0) * nw, nw, lane, valid);
-    };
-    // SmoothGrad noise of the two ext rows a wave owns in a block, generated together (two
-    // interleaved Philox chains). Element group g = (row's first element) / 4 + lane < 2^32 (host
-    // check), so wam_normal4_x2 reproduces wam_normal4's stream; lanes past the row are never stored.
-    auto noise2 = [&](float (&za)[4], float (&zb)[4], int sra, int srb) {
-      if constexpr (NOISE) {
-        const uint32_t rowg = (uint32_t)(ch * nh) * (uint32_t)nw / 4u + (uint32_t)lane;
-        const uint32_t nw4 = (uint32_t)nw / 4u;
-        wam_normal4_x2(rowg + (uint32_t)(sra >= 0 ? sra : 0) * nw4, rowg + (uint32_t)(srb >= 0 ? srb : 0) * nw4,
-                       (uint32_t)(img + nz.image_base), (uint32_t)smp, nz.k0, nz.k1, za, zb);
-      }
     };
     // horizontal pass of ext row e into its ring slot (nzr: its noise, from noise2)
     auto hrow = [&](RowRegs<4, 1> (&fr)[NCH], int sr, int e, const float (&nzr)[4]) {
@@ -297,21 +299,32 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
       noise2(za, zb, spro, spro);
       hrow(fp, spro, wv - p, za);
     }
+    // the noise of block b + 1's rows is generated between the barrier and block b's vertical
+    // pass: pure ALU work that overlaps the vertical pass's LDS reads (its rows are known: they
+    // were fetched D - 1 blocks earlier)
+    float Z[D][2][4];
+#pragma unroll
+    for (int u = 0; u < D; ++u)
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) Z[u][r][k] = 0.f;
+    noise2(Z[0][0], Z[0][1], S[0][0], S[0][1]);
     for (int b0 = 0; b0 < nb; b0 += D) {
 #pragma unroll
       for (int u = 0; u < D; ++u) {
         const int b = b0 + u;
+        const int un = (u + 1) % D;  // static after unrolling
         if (b < nb) {  // workgroup-uniform
-          float za[4] = {0.f, 0.f, 0.f, 0.f}, zb[4] = {0.f, 0.f, 0.f, 0.f};
-          noise2(za, zb, S[u][0], S[u][1]);
-          hrow(F[u][0], S[u][0], 16 * b + 2 * wv, za);
-          hrow(F[u][1], S[u][1], 16 * b + 2 * wv + 1, zb);
+          hrow(F[u][0], S[u][0], 16 * b + 2 * wv, Z[u][0]);
+          hrow(F[u][1], S[u][1], 16 * b + 2 * wv + 1, Z[u][1]);
         }
         // refill: block b + D (past the plane: clamped rows, never consumed)
         fetch(F[u][0], S[u][0], 16 * (b + D) + 2 * wv);
         fetch(F[u][1], S[u][1], 16 * (b + D) + 2 * wv + 1);
         if (b < nb) {
           __syncthreads();  // ring rows of block b complete
+          if (b + 1 < nb) noise2(Z[un][0], Z[un][1], S[un][0], S[un][1]);
           vblock(b);
           __syncthreads();  // ring slots free for block b + 1
         }
@@ -364,13 +377,8 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
       for (int c = 0; c < NCH; ++c) fr[c].fetch(src + c * in_plane + (int64_t)rr * nw, nw, lane, valid);
     };
     f2 rv[CPL][L];  // ring: (lo, hi) of ext row t in slot t % L
-    auto consume = [&](RowRegs<4, 1> (&fr)[NCH], int sr, int slot) {
-      // the noise depends only on (row, lane): generate it before touching the fetched row so the
-      // Philox work overlaps the row's load latency instead of following its vmcnt wait
-      float nzr[4];
-      if constexpr (NOISE)
-        make_noise<1>(nzr, nw, lane, (ch * nh + (sr >= 0 ? sr : 0)) * (int64_t)nw, sg, img + nz.image_base, smp,
-                      nz.k0, nz.k1, sr >= 0);
+    // nzr: the row's noise from noise2 (rows are noised in pairs: ext rows t, t + 1 for even t)
+    auto consume = [&](RowRegs<4, 1> (&fr)[NCH], int sr, int slot, const float (&nzr)[4]) {
       RowRegs<4, 1> m = fr[0];
       if constexpr (NCH > 1) {
 #pragma unroll
@@ -382,7 +390,9 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
         for (int u = 0; u < 4; ++u) m.v[u] *= inv;
       }
       if constexpr (NOISE) {
-        m.commit(lds, lane, nzr, sg);
+        // zero rows and the lanes past the row (their unguarded commit lands on the zero-mode pad
+        // slots) stay zero: fma(0, z, 0)
+        m.commit(lds, lane, nzr, (sr >= 0 && lane * 4 < nw) ? sg : 0.f);
       } else {
         m.commit(lds, lane, nullptr);
       }
@@ -444,10 +454,12 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
       for (int u = 0; u < NBL - 1; ++u) fetch(f[u], srow[u], u);
       // prologue: ext rows 0 .. L-3 fill ring slots 0 .. L-3
+      float za[4] = {0.f, 0.f, 0.f, 0.f}, zb[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < L - 2; ++t) {
         fetch(f[(t + NBL - 1) % NBL], srow[(t + NBL - 1) % NBL], t + NBL - 1);
-        consume(f[t % NBL], srow[t % NBL], t);
+        if (!(t & 1)) noise2(za, zb, srow[t % NBL], srow[(t + 1) % NBL]);  // row t + 1 is fetched
+        consume(f[t % NBL], srow[t % NBL], t, (t & 1) ? zb : za);
       }
       // steady state: GRPL ext rows per iteration; t = base + u with base = L-2 (mod GRPL), so
       // t % L and t % NBL are compile-time constants; a partial last group computes output rows
@@ -457,7 +469,9 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
         for (int u = 0; u < GRPL; ++u) {
           const int t = base + u;
           fetch(f[(L - 2 + u + NBL - 1) % NBL], srow[(L - 2 + u + NBL - 1) % NBL], t + NBL - 1);
-          consume(f[(L - 2 + u) % NBL], srow[(L - 2 + u) % NBL], (L - 2 + u) % L);
+          if (!(u & 1))  // t even (L - 2 and GRPL are even): rows t, t + 1 noised together
+            noise2(za, zb, srow[(L - 2 + u) % NBL], srow[(L - 2 + u + 1) % NBL]);
+          consume(f[(L - 2 + u) % NBL], srow[(L - 2 + u) % NBL], (L - 2 + u) % L, (u & 1) ? zb : za);
           // after odd u: output row (t - (L-1)) / 2 from ext rows t-L+1 .. t = slots (u-1+k) % L
           if (u & 1) emit(i0 + (t - (L - 1)) / 2, (u - 1) % L);
         }
@@ -484,57 +498,70 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     const bool lastlvl = l == g.J - 1;
     const int mode = g.mode;
     float mx[4] = {0.f, 0.f, 0.f, 0.f};
-    const int nrb = kPT / mw;  // mw <= kPT (geom_ok)
+    // thread (rb, j): output column j, output rows [i0, i1) of row block rb; a block filters
+    // 2R + L - 2 ext rows for R outputs, so blocks are kept >= L rows long where the level allows
+    int nrb = kPT / mw;  // mw <= kPT (geom_ok)
+    if (nrb > max(1, mh / L)) nrb = max(1, mh / L);
     const int rb = tid / mw, j = tid - rb * mw;
     if (rb < nrb) {
       const int R2 = (mh + nrb - 1) / nrb;
       const int i0 = rb * R2;
       const int i1 = min(mh, i0 + R2);
       if (i0 < i1) {
-        int cidx[L];
+        // ext column 2j - p + k of the level: a zero-mode tap outside the row gets a zero filter
+        // pair and a clamped address (fma(0, x, acc) = acc: the sums of the skipped taps)
+        int cofs[L];
+        f2 fk[L];
 #pragma unroll
-        for (int k = 0; k < L; ++k) cidx[k] = wam_ext_index(2 * j - p + k, sw, mode);
+        for (int k = 0; k < L; ++k) {
+          const int c = wam_ext_index(2 * j - p + k, sw, mode);
+          cofs[k] = c >= 0 ? c : 0;
+          fk[k] = c >= 0 ? fh2[k] : f2{0.f, 0.f};
+        }
         const int er0 = 2 * i0 - p;
-        auto hrow = [&](int t, float& lo, float& hi) {
-          const int sr = wam_ext_index(er0 + t, sh, mode);
-          float a = 0.f, d = 0.f;
+        // (lo, hi) of ext row t of this block, packed FMAs in tap order (zero-mode rows outside
+        // the level: (0, 0))
+        auto hrow = [&](int t) {
+          const int sr = row_src(er0 + t, sh, mode);
+          f2 acc = f2{0.f, 0.f};
           if (sr >= 0) {
             const float* s = lsrc + sr * sw;
 #pragma unroll
             for (int k = 0; k < L; ++k) {
-              const float x = cidx[k] >= 0 ? s[cidx[k]] : 0.f;
-              a = fmaf(flo[k], x, a);
-              d = fmaf(fhi[k], x, d);
+              const float x = s[cofs[k]];
+              acc = __builtin_elementwise_fma(fk[k], f2{x, x}, acc);
             }
           }
-          lo = a;
-          hi = d;
+          return acc;
         };
-        float rl[L], rh[L];
+        // ring: ext row t in slot t % L; output row i0 + ii reads ext rows 2ii .. 2ii + L - 1,
+        // i.e. slots (2u + k) % L for ii = ib + u with ib a multiple of L / 2 (static indices)
+        f2 r[L];
 #pragma unroll
-        for (int t = 0; t < L - 2; ++t) hrow(t, rl[t], rh[t]);
-        for (int i = i0; i < i1; ++i) {
-          const int t = 2 * (i - i0) + L - 2;
-          hrow(t, rl[L - 2], rh[L - 2]);
-          hrow(t + 1, rl[L - 1], rh[L - 1]);
-          float a = 0.f, h = 0.f, v = 0.f, d = 0.f;
+        for (int t = 0; t < L - 2; ++t) r[t] = hrow(t);
+        for (int ib = 0; i0 + ib < i1; ib += L / 2) {
 #pragma unroll
-          for (int k = 0; k < L; ++k) {
-            a = fmaf(flo[k], rl[k], a);
-            h = fmaf(fhi[k], rl[k], h);
-            v = fmaf(flo[k], rh[k], v);
-            d = fmaf(fhi[k], rh[k], d);
-          }
-          const int64_t idx = (int64_t)i * mw + j;
-          if (lastlvl) bo.put(g, g.off_a, bn, idx, a, mx[3]);
-          else ldst[idx] = a;
-          bo.put(g, g.off[l][0], bn, idx, h, mx[0]);
-          bo.put(g, g.off[l][1], bn, idx, v, mx[1]);
-          bo.put(g, g.off[l][2], bn, idx, d, mx[2]);
+          for (int u = 0; u < L / 2; ++u) {
+            const int ii = ib + u;
+            const int i = i0 + ii;
+            if (i < i1) {
+              r[(2 * u + L - 2) % L] = hrow(2 * ii + L - 2);
+              r[(2 * u + L - 1) % L] = hrow(2 * ii + L - 1);
+              // (a, h) = sum (flo, fhi)[k] * lo_k, (v, d) = sum (flo, fhi)[k] * hi_k in tap order
+              f2 ah = f2{0.f, 0.f}, vd = f2{0.f, 0.f};
 #pragma unroll
-          for (int k = 0; k < L - 2; ++k) {
-            rl[k] = rl[k + 2];
-            rh[k] = rh[k + 2];
+              for (int k = 0; k < L; ++k) {
+                const f2 q = r[(2 * u + k) % L];
+                ah = __builtin_elementwise_fma(fh2[k], f2{q.x, q.x}, ah);
+                vd = __builtin_elementwise_fma(fh2[k], f2{q.y, q.y}, vd);
+              }
+              const int64_t idx = (int64_t)i * mw + j;
+              if (lastlvl) bo.put(g, g.off_a, bn, idx, ah.x, mx[3]);
+              else ldst[idx] = ah.x;
+              bo.put(g, g.off[l][0], bn, idx, ah.y, mx[0]);
+              bo.put(g, g.off[l][1], bn, idx, vd.x, mx[1]);
+              bo.put(g, g.off[l][2], bn, idx, vd.y, mx[2]);
+            }
           }
         }
       }
@@ -781,15 +808,19 @@ int coop_lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap) {
   return (int)(llcap + bcap);
 }
 
-bool coop_ok(const wam_plan* p, int nw0) {
+// The noisy analysis defaults to the wave-chunk form: it re-noises the L-2 halo rows of each
+// wave's chunk but runs without the two workgroup barriers per 8 output rows, 8-10 % faster at the
+// c2 shape (profiles/r02f_plane_ab.log); the clean analysis and the maps pass keep COOP.
+bool coop_ok(const wam_plan* p, int nw0, bool noisy = false) {
   if (p->flags & WAM_PLAN_NO_COOP) return false;
+  if (noisy && !(p->flags & WAM_PLAN_FORCE_COOP)) return false;
   if (p->lout[0][1] > 128 || p->pad > kCoopPadL) return false;
   int rowlds, llcap;
   return (int64_t)coop_lds_floats(p, nw0, rowlds, llcap) * 4 <= kTwoWgLds || (p->flags & WAM_PLAN_FORCE_COOP);
 }
 
-int lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap) {
-  if (coop_ok(p, nw0)) return coop_lds_floats(p, nw0, rowlds, llcap);
+int lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap, bool noisy = false) {
+  if (coop_ok(p, nw0, noisy)) return coop_lds_floats(p, nw0, rowlds, llcap);
   rowlds = kPadL + 256 + 8;  // commit covers 256 samples; pads <= p + 2 <= 20 fit behind them
   if (rowlds < kPadL + nw0 + p->pad + 4) rowlds = kPadL + nw0 + p->pad + 4;
   rowlds = (rowlds + 3) & ~3;
@@ -814,7 +845,7 @@ bool geom_ok(const wam_plan* p, int nw0, int nh0) {
   return (int64_t)lds_floats(p, nw0, rowlds, llcap) * 4 <= kPlaneLdsCap;
 }
 
-PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items_total) {
+PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items_total, bool noisy = false) {
   PlaneGeom g{};
   g.J = p->levels;
   g.mode = mode;
@@ -832,8 +863,8 @@ PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items
   g.nbands = p->nbands;
   g.items_total = items_total;
   g.maps_item = p->band_off[p->nbands];
-  lds_floats(p, nw0, g.rowlds, g.llcap);
-  g.coop = coop_ok(p, nw0);
+  lds_floats(p, nw0, g.rowlds, g.llcap, noisy);
+  g.coop = coop_ok(p, nw0, noisy);
   g.sample_fast = 1;
   return g;
 }
@@ -895,9 +926,9 @@ int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in
   const int nw0 = (int)(adjoint ? p->rec_shape[1] : p->lin[0][1]);
   const int mode = adjoint ? WAM_MODE_ZERO : p->mode;
   const float* filt = p->d_filt + (adjoint ? WAM_F_ADJ_LO : WAM_F_ANA_LO) * p->L;
-  const PlaneGeom g = make_geom(p, nh0, nw0, mode, items);
+  const PlaneGeom g = make_geom(p, nh0, nw0, mode, items, nz != nullptr);
   int rowlds, llcap;
-  const int lds_bytes = lds_floats(p, nw0, rowlds, llcap) * 4;
+  const int lds_bytes = lds_floats(p, nw0, rowlds, llcap, nz != nullptr) * 4;
   const double in_planes = nz ? (double)nz->images * nz->channels : (double)items;
   const double bytes = 4.0 * (in_planes * nh0 * nw0 + (double)items * p->band_off[p->nbands]);
   if (nz) {
