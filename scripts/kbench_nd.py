@@ -19,10 +19,13 @@ from wam_amd import plan as P  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--only", default=None, help="c3 or c5")
     args = ap.parse_args()
     torch.manual_seed(0)
     for tag, dim, shape, J, wav, mode, B in [("c3 1D", 1, (80000,), 5, "db6", "reflect", 6400),
                                              ("c5 3D", 3, (128, 128, 128), 2, "haar", "symmetric", 400)]:
+        if args.only and not tag.startswith(args.only):
+            continue
         p = P.get_plan(dim, shape, J, wav, mode, "cuda")
         x = torch.randn((B,) + shape, device="cuda")
         run(f"{tag} wavedec B={B}", lambda: p.wavedec(x), args.iters)

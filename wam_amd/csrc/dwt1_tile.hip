@@ -40,7 +40,9 @@ int lds_opt_in(const void* kern, int bytes) {
 
 constexpr int kT1 = 512;          // threads per workgroup (analysis)
 constexpr int kT1S = 256;         // threads per workgroup (synthesis)
-constexpr int kTile0 = 4096;      // finest-level outputs per tile (source window ~2 x this)
+constexpr int kTile0 = 4096;      // synthesis: half the level-0 outputs of a tile
+constexpr int kTileA = 4096;      // analysis: finest-level outputs per tile (source window ~2 x this)
+constexpr int kAnaWgs = 2;        // analysis: persistent workgroups per CU
 constexpr int kLds1Cap = 80 * 1024;  // two workgroups per CU
 
 struct Dwt1Geom {
@@ -649,7 +651,7 @@ Dwt1Geom make_geom1(const wam_plan* p, int n, int mode, int64_t items) {
   }
   g.off_a = p->band_off[0];
   g.items = items;
-  g.tile_j = std::max(1, kTile0 >> (p->levels - 1));
+  g.tile_j = std::max(1, kTileA >> (p->levels - 1));
   int tiles = 1;
   for (int l = 0; l < p->levels; ++l) {
     const int T = g.tile_j << (p->levels - 1 - l);
@@ -746,7 +748,7 @@ int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in,
     WAM_HIP_CHECK(hipGetDevice(&dev));
     int cus = 256;
     WAM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const int64_t grid = std::min<int64_t>(units, 2LL * cus);
+    const int64_t grid = std::min<int64_t>(units, (int64_t)kAnaWgs * cus);
     WamTimer tm(st, "k_dwt1_ana_int", bytes * (double)(t_hi - t_lo) / g.tiles);
     switch (p->L) {
 #define WAM_D1AI(LL)                                                                                            \
@@ -775,7 +777,7 @@ int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in,
     WAM_HIP_CHECK(hipGetDevice(&dev));
     int cus = 256;
     WAM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const int64_t grid = std::min<int64_t>(nb_blocks, 2LL * cus);
+    const int64_t grid = std::min<int64_t>(nb_blocks, (int64_t)kAnaWgs * cus);
     WamTimer tm(st, "k_dwt1_ana_p", bytes * (double)(g.tiles - (t_hi - t_lo)) / g.tiles);
     switch (p->L) {
 #define WAM_D1AP(LL)                                                                                           \
