@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(256) k_dwt2_ana(const float* __restrict__ in, 
   __shared__ __attribute__((aligned(16))) float seg[4][SEGW + 2];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int64_t gw = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t gw = wam_xcd_block(blockIdx.x, gridDim.x) * 4 + wv;
   if (gw >= total_waves) return;
   // strip fastest: the strips of one (plane, row chunk) -- which fetch the same source rows --
   // are waves of one workgroup (one CU, one XCD L2) instead of landing on different XCDs
@@ -134,7 +134,7 @@ __global__ void __launch_bounds__(256) k_dwt2_syn(const float* __restrict__ A, c
   __shared__ __attribute__((aligned(16))) float4 xch[4][64];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int64_t gw = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t gw = wam_xcd_block(blockIdx.x, gridDim.x) * 4 + wv;
   if (gw >= total_waves) return;
   // strip fastest: the strips of one (plane, row chunk) -- which fetch the same source rows --
   // are waves of one workgroup (one CU, one XCD L2) instead of landing on different XCDs

@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, 
   __shared__ __attribute__((aligned(16))) float rows[kWaves][kRowLds];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int64_t gw = (int64_t)blockIdx.x * kWaves + wv;
+  const int64_t gw = wam_xcd_block(blockIdx.x, gridDim.x) * kWaves + wv;
   if (gw >= total_waves) return;
   // strip fastest: the strips of one (plane, row chunk) -- which fetch the same source rows --
   // are waves of one workgroup (one CU, one XCD L2) instead of landing on different XCDs
@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
   __shared__ __attribute__((aligned(16))) float rows[kWaves][C][kRowLds];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int64_t gw = (int64_t)blockIdx.x * kWaves + wv;
+  const int64_t gw = wam_xcd_block(blockIdx.x, gridDim.x) * kWaves + wv;
   if (gw >= total_waves) return;
   // strip fastest: the strips of one (plane, row chunk) -- which fetch the same source rows --
   // are waves of one workgroup (one CU, one XCD L2) instead of landing on different XCDs

@@ -2,6 +2,15 @@
 #pragma once
 #include "common.hpp"
 
+// Logical workgroup id under which consecutive ids run on one XCD. Workgroup b is observed to land
+// on XCD b % 8 (round robin; not a contract, so only locality depends on it): the bijection maps
+// each XCD's physical blocks onto one contiguous logical range, so neighbouring work items (the row
+// chunks and column strips of a plane, which re-read each other's halo rows) share an L2.
+__device__ __forceinline__ int64_t wam_xcd_block(int64_t bid, int64_t nwg) {
+  const int64_t q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+}
+
 // generic per-axis kernels (dwt_axis.hip)
 int launch_analysis_axis(const float* in, float* lo, float* hi, int64_t outer, int n, int m, int64_t inner,
                          int padl, int mode, const float* flo, const float* fhi, int L, hipStream_t st);
