@@ -170,7 +170,7 @@ def workload(name):
     raise ValueError(name)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--gpus", type=int, default=1)
@@ -187,7 +187,7 @@ def parse():
     ap.add_argument("--extras", default="auto", choices=["auto", "off"], help="c2 parity / variants / ceilings")
     ap.add_argument("--dist-axis", default=None, choices=["auto", "samples", "images"])
     ap.add_argument("--wam-probe", action="store_true", help=argparse.SUPPRESS)  # PMC child run
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 # ============================================================================ explainer

@@ -131,6 +131,35 @@ def test_legacy_noise_stream_matches_reference_loop():
         assert np.array_equal((x + torch.tensor(got[s])).numpy(), ref[s].numpy())
 
 
+def _np_state_equal(a, b):
+    return a[0] == b[0] and np.array_equal(a[1], b[1]) and a[2:] == b[2:]
+
+
+@pytest.mark.parametrize("shape,items,samples", [((2, 5, 5), 3, 4), ((7,), 2, 5), ((3, 4, 4, 4), 1, 3)])
+def test_legacy_noise_device_replay_bit_exact(shape, items, samples):
+    """engine.LegacyNoise (unscaled stream drawn once, scaled on the device in fp64, cast to fp32)
+    equals the reference loop np.random.normal(0, sigma_i, shape).astype(float32) bit for bit, for
+    full and partial (sharded) sample / item ranges, on a cache miss and a cache hit, and leaves the
+    global numpy RNG in the reference's end state both times (odd item sizes: the polar method's
+    cached second value carries across items)."""
+    engine.clear_noise_cache()
+    sig = [0.1 + 0.37 * i for i in range(items)]
+    want = dict(engine.legacy_noise(sig, shape, 42, list(range(samples))))
+    end = np.random.get_state()
+    for attempt in range(2):  # miss, then hit
+        np.random.seed(7)  # a different state: the replay must not depend on it
+        ln = engine.LegacyNoise(np.asarray(sig), shape, 42, samples, "cpu")
+        assert _np_state_equal(np.random.get_state(), end)
+        full = ln.chunk(0, samples).numpy()
+        for s in range(samples):
+            assert np.array_equal(full[s], want[s]), (attempt, s)
+        part = ln.chunk(1, samples - 1, items - 1, items).numpy()
+        for k in range(samples - 1):
+            assert np.array_equal(part[k], want[1 + k][items - 1:items])
+    assert len(engine._GAUSS_CACHE) == 1
+    engine.clear_noise_cache()
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("n", [1, 3, 25, 64])
 def test_shard_ranges_partition(world, n):

@@ -10,6 +10,7 @@ one group per call).
 Only the input gradient is computed (torch.autograd.grad): the reference's parameter-.grad
 accumulation side effect is not reproduced.
 """
+import collections
 import contextlib
 
 import numpy as np
@@ -134,6 +135,59 @@ def legacy_noise(sigmas, item_shape, seed, samples, n_total=None):
             arr[i] = np.random.normal(0, sg, tuple(item_shape)).astype(np.float32)
         if s in want:
             yield s, arr
+
+
+# (seed, item numel, items, samples, device) -> (device float64 [samples, items, numel] standard
+# normals, numpy global RNG state after them); least recently used entries go first
+_GAUSS_CACHE = collections.OrderedDict()
+GAUSS_CACHE_BYTES = 4 << 30
+
+
+def clear_noise_cache():
+    _GAUSS_CACHE.clear()
+
+
+class LegacyNoise:
+    """The reference's noise stream (lib/wam_2D.py:385-403, lib/wam_1D.py, lib/wam_3D.py):
+    np.random.seed(seed), then for every sample s and item i in order
+    np.random.normal(0, sigma_i, item_shape) in float64, cast to float32 -- replayed on the device.
+
+    numpy's legacy normal is ``loc + scale * gauss`` over the unscaled MT19937 / polar sequence, and
+    that sequence depends only on (seed, item size, items, samples), not on the images. It is drawn
+    once with np.random.standard_normal (the same generator calls in the same order), kept on the
+    device in float64 (bounded LRU cache, GAUSS_CACHE_BYTES), and each call scales it there:
+    float32(sigma_i * g) is the reference's value bit for bit (IEEE fp64 product, round-to-nearest
+    cast; 0.0 + v = v). The global numpy RNG is left where the reference leaves it: after all
+    n_samples samples (a cache hit restores that state with np.random.set_state)."""
+
+    def __init__(self, sigmas, item_shape, seed, n_samples, device):
+        numel = int(np.prod(item_shape))
+        items = len(sigmas)
+        key = (int(seed), numel, items, int(n_samples), str(device))
+        ent = _GAUSS_CACHE.get(key)
+        if ent is None:
+            np.random.seed(seed)
+            g = np.empty((n_samples, items, numel), dtype=np.float64)
+            for s in range(n_samples):
+                for i in range(items):
+                    g[s, i] = np.random.standard_normal(numel)
+            ent = (torch.from_numpy(g).to(device), np.random.get_state())
+            if g.nbytes <= GAUSS_CACHE_BYTES:
+                _GAUSS_CACHE[key] = ent
+                while sum(v[0].numel() * 8 for v in _GAUSS_CACHE.values()) > GAUSS_CACHE_BYTES:
+                    _GAUSS_CACHE.popitem(last=False)
+        else:
+            _GAUSS_CACHE.move_to_end(key)
+            np.random.set_state(ent[1])
+        self.g = ent[0]
+        self.sigma = torch.tensor([float(v) for v in sigmas], dtype=torch.float64, device=self.g.device)
+        self.shape = tuple(item_shape)
+
+    def chunk(self, s0, cnt, i_lo=0, i_hi=None):
+        """float32 noise [cnt, items, *item_shape] of samples s0 .. s0+cnt-1, items [i_lo, i_hi)."""
+        i_hi = self.g.shape[1] if i_hi is None else i_hi
+        z = self.g[s0:s0 + cnt, i_lo:i_hi] * self.sigma[i_lo:i_hi, None]
+        return z.float().view((cnt, i_hi - i_lo) + self.shape)
 
 
 # ------------------------------------------------------------------------------ distribution

@@ -11,7 +11,7 @@ sample_batch, autocast_dtype, dist).
 import numpy as np
 import torch
 
-from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, legacy_noise, model_device,
+from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, LegacyNoise, model_device,
                      require_gpu_device)
 from .melspec import kernel_supported, mel_adjoint, mel_forward, melspec_db
 from .plan import accumulate_f32, get_plan, item_sigma, noise_add, trapz_stream
@@ -182,19 +182,16 @@ class WaveletAttribution1D(BaseWAM1D):
         shard = Shard(self.dist)
         s_lo, s_hi = shard.range(self.n_samples)
         group = auto_group(self.model, n, self.sample_batch)
-        noise_it = None
+        legacy = None
         if self.noise == "numpy":
-            noise_it = legacy_noise([float(v) for v in sigma.cpu().numpy()], (w,), self.random_seed,
-                                    list(range(s_lo, s_hi)))
+            legacy = LegacyNoise(sigma.cpu().numpy(), (w,), self.random_seed, self.n_samples, dev)
         # accumulators exist before the loop: a rank whose sample range is empty (n_samples <
         # world size) still joins the all-reduce with zeros
         self._mel_shape = (n, 1, plan.rec_shape[0] // (self.n_fft // 2) + 1, self.n_mels)
         mel_acc = torch.zeros(int(np.prod(self._mel_shape)), dtype=torch.float32, device=dev)
         c_acc = torch.zeros(n * plan.coeff_numel, dtype=torch.float32, device=dev)
         for s0, cnt in chunks(s_lo, s_hi, group):
-            host = None
-            if noise_it is not None:
-                host = torch.from_numpy(np.stack([next(noise_it)[1] for _ in range(cnt)])).to(dev)
+            host = None if legacy is None else legacy.chunk(s0, cnt)
             noisy = noise_add(x, sigma, cnt, n, w, w, seed=self.random_seed, sample_base=s0, host_noise=host)
             flat = plan.wavedec(noisy.view(cnt * n, w))
             g_mel, cg = self._grads(plan, flat, cnt * n, y, cnt, n)

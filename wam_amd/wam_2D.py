@@ -32,7 +32,7 @@ import torch.nn.functional as F
 
 from . import frames
 from .constants import WaveletDetailTuple2d
-from .engine import (GradModel, Shard, auto_group, chunks, ig_weights, legacy_noise, model_device,
+from .engine import (GradModel, LegacyNoise, Shard, auto_group, chunks, ig_weights, model_device,
                      require_gpu_device, wam_group)
 from .plan import (CAP_ADJOINT_MAPS, CAP_NOISY_WAVEDEC, disentangle_scales, frame_accumulate, frame_trapz,
                    get_plan, item_sigma, noise_add, reproject_scales, subband_maps)
@@ -374,17 +374,14 @@ class WaveletAttribution2D(BaseWAM2D):
         # parity mode streams the host-generated legacy noise one model group at a time
         wgroup = group if self.noise == "numpy" else self._wam_group(plan, n, c, group, s_hi - s_lo)
         frame = torch.zeros(n * rh * rw, dtype=torch.float64, device=dev)
-        noise_it = None
+        legacy = None
         if self.noise == "numpy":
-            noise_it = legacy_noise([float(v) for v in sigma_all.cpu().numpy()], (c, h, w), self.random_seed,
-                                    list(range(s_lo, s_hi)))
+            legacy = LegacyNoise(sigma_all.cpu().numpy(), (c, h, w), self.random_seed, self.n_samples, dev)
         rec = plan.rec_shape
         last = None
         for s0, cnt in chunks(s_lo, s_hi, wgroup):
-            if noise_it is not None:
-                arr = np.stack([next(noise_it)[1][i_lo:i_hi] for _ in range(cnt)])
-                host = torch.from_numpy(arr).pin_memory().to(dev, non_blocking=True)
-                noisy = noise_add(xs, sigma, cnt, n, item, item, host_noise=host)
+            if legacy is not None:
+                noisy = noise_add(xs, sigma, cnt, n, item, item, host_noise=legacy.chunk(s0, cnt, i_lo, i_hi))
                 flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
             elif plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
                 flat = plan.wavedec_noisy(xs, sigma, cnt, n, c, self.random_seed, s0, image_base=i_lo)

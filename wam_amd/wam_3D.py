@@ -19,7 +19,7 @@ import torch
 
 from . import frames
 from .constants import KEYS3
-from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, legacy3d_weights, legacy_noise,
+from .engine import (LegacyNoise, Shard, auto_group, chunks, ig_weights, input_gradient, legacy3d_weights,
                      model_device, require_gpu_device)
 from ._lib import check, lib, ptr, stream_of
 from .plan import cube_accumulate, get_plan, item_sigma, noise_add, subband_maps
@@ -285,21 +285,19 @@ class WaveletAttribution3D(BaseWAM3D):
         shard = Shard(self.dist)
         s_lo, s_hi = shard.range(self.n_samples)
         group = 1 if y is None else auto_group(self.model, n, self.sample_batch, cap_items=32)
-        noise_it = None
+        legacy = None
         if self.noise == "numpy":
-            noise_it = legacy_noise([float(v) for v in sigma.cpu().numpy()], sp, self.random_seed,
-                                    list(range(s_lo, s_hi)))
+            legacy = LegacyNoise(sigma.cpu().numpy(), sp, self.random_seed, self.n_samples, dev)
         acc = torch.zeros(n * S ** 3, dtype=torch.float32, device=dev)
         ns = self.n_samples
         for s0, cnt in chunks(s_lo, s_hi, group):
             host = None
-            if noise_it is not None:
-                arr = np.stack([next(noise_it)[1] for _ in range(cnt)])  # [cnt, n, *sp]
-                if c > 1:
-                    full = np.zeros((cnt, n, c) + sp, dtype=np.float32)
-                    full[:, :, 0] = arr
-                    arr = full
-                host = torch.from_numpy(np.ascontiguousarray(arr)).to(dev)
+            if legacy is not None:
+                host = legacy.chunk(s0, cnt)  # [cnt, n, *sp]
+                if c > 1:  # the reference noises channel 0 only
+                    full = torch.zeros((cnt, n, c) + sp, dtype=torch.float32, device=dev)
+                    full[:, :, 0] = host
+                    host = full
             noisy = noise_add(x, sigma, cnt, n, c * vol, vol, seed=self.random_seed, sample_base=s0, host_noise=host)
             flat = plan.wavedec(noisy.view((cnt * n * c,) + sp))
             cg = self._grads(plan, flat, cnt * n * c, y, cnt, n, c)
