@@ -639,6 +639,19 @@ def main():
 
     log("timed: %.1f ms per step" % (dt / args.steps * 1e3))
     secondary = {}
+    if wl.kw.get("noise", "numpy") == "numpy" and wl.kw.get("method") == "smooth":
+        # parity-mode noise: the legacy numpy stream is drawn on the host once per (seed, shape,
+        # batch) and replayed from the device afterwards (engine.LegacyNoise); a first ("cold")
+        # call pays the host generation
+        engine.clear_noise_cache()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ex(xd, y)
+        torch.cuda.synchronize(dev)
+        secondary["noise_cache"] = {
+            "cold_call_ms": round((time.perf_counter() - t0) * 1e3, 2), "warm_call_ms": round(dt / args.steps * 1e3, 2),
+            "what": "timed calls replay the reference's legacy numpy noise stream from the device (drawn once per "
+                    "seed / shape / batch, scaled per call, bit-exact); cold_call_ms = one call after clearing it"}
     if world > 1:
         secondary["collectives"] = collectives_timing(wl, dev, world, axis)
         exw = build_explainer(wl, dev, args, dist_on=False)  # each rank its own batch, no collective
