@@ -227,6 +227,26 @@ def test_noisy_wavedec_equals_noise_then_wavedec(wam, wav, J):
     assert torch.equal(fused, ref)
 
 
+@pytest.mark.parametrize("shape,J,mode,S,N", [((128, 128, 128), 2, "symmetric", 2, 3), ((16, 12, 20), 1, "reflect", 3, 2),
+                                              ((8, 16, 24), 2, "zero", 5, 1), ((6, 10, 4), 1, "symmetric", 2, 4)])
+def test_noisy_haar3_equals_noise_then_wavedec(wam, shape, J, mode, S, N):
+    """3D Haar analysis with the SmoothGrad noise fused on the load (single-channel volumes, the
+    samples of a volume chunk in consecutive workgroups) vs wam_noise_add + the block kernel:
+    bit-identical, with a sample base and a non-zero seed; channels != 1 is refused."""
+    p = wam.get_plan(3, shape, J, "haar", mode, "cuda")
+    assert p.caps & wam.CAP_NOISY_WAVEDEC
+    torch.manual_seed(12)
+    vol = shape[0] * shape[1] * shape[2]
+    x = torch.randn((N, 1) + shape, device="cuda")
+    sigma = wam.item_sigma(x, vol, vol, 0.3)
+    fused = p.wavedec_noisy(x, sigma, S, N, 1, seed=77, sample_base=3)
+    noisy = wam.noise_add(x, sigma, S, N, vol, vol, seed=77, sample_base=3)
+    ref = p.wavedec(noisy.view((S * N,) + shape))
+    assert torch.equal(fused, ref)
+    with pytest.raises(Exception):
+        p.wavedec_noisy(torch.randn((N, 2) + shape, device="cuda"), sigma, S, N, 2, seed=77)
+
+
 @pytest.mark.parametrize("wav,shape,J,C", [("db4", (224, 224), 3, 3), ("haar", (224, 224), 3, 3),
                                            ("sym8", (128, 96), 2, 1), ("db6", (225, 223), 3, 3),
                                            ("db2", (64, 300), 2, 1)])

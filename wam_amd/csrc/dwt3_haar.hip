@@ -9,6 +9,7 @@
 // Arithmetic follows the per-axis kernels exactly (W then H then D; fmaf chains starting at 0),
 // so results are bit-identical to the generic path.
 #include "kernels.hpp"
+#include "rng.hpp"
 
 namespace {
 
@@ -77,17 +78,41 @@ __device__ __forceinline__ void haar3_inv(const float (&c)[8], const float (&r)[
     for (int x = 0; x < 2; ++x) syn2(h[0][y][x], h[1][y][x], r, v[0][y][x], v[1][y][x]);
 }
 
-template <int J>
+// NOISE: SmoothGrad sample generation fused into the load (single-channel volumes): output item
+// s * images + i is the transform of x_i + sigma_i * N(0,1) with the Philox stream of
+// wam_noise_add (counter (sample_base + s, image_base + i, element / 4)); a B-wide row of a block
+// is one (B = 4) or half a (B = 2) group of 4 elements, so noise costs one Philox call per row.
+// Work order (NOISE): workgroup w takes sample w % S of a 256-block chunk of image w / S, so the S
+// samples of a chunk are consecutive (XCD-swizzled) workgroups and read the clean chunk from one L2.
+template <int J, bool NOISE>
 __global__ void __launch_bounds__(kT3) k_haar3_ana(const float* __restrict__ in, float* __restrict__ coeffs,
-                                                  const float* __restrict__ filt, Haar3Geom g, int64_t blocks) {
+                                                  const float* __restrict__ filt, Haar3Geom g, int64_t blocks,
+                                                  WamNoise nz, int64_t S) {
   constexpr int B = 1 << J;
-  const int64_t t = (int64_t)blockIdx.x * kT3 + threadIdx.x;
-  if (t >= blocks) return;
   const int64_t bw = g.W / B, bh = g.H / B, bd = g.D / B;
-  const int64_t bx = t % bw, by = (t / bw) % bh, bz = (t / (bw * bh)) % bd, item = t / (bw * bh * bd);
+  const int64_t nb = bw * bh * bd;  // blocks per volume
+  int64_t t, item, src_item, smp = 0;
+  float sg = 0.f;
+  if constexpr (NOISE) {
+    const int64_t nc = (nb + kT3 - 1) / kT3;  // workgroup chunks per volume
+    const int64_t w = wam_xcd_block(blockIdx.x, gridDim.x);
+    const int64_t s = w % S, rest = w / S, i = rest / nc;
+    t = (rest % nc) * kT3 + threadIdx.x;
+    if (t >= nb || i >= nz.images) return;
+    src_item = i;
+    item = s * nz.images + i;
+    smp = nz.sample_base + s;
+    sg = nz.sigma[i];
+  } else {
+    const int64_t tt = (int64_t)blockIdx.x * kT3 + threadIdx.x;
+    if (tt >= blocks) return;
+    t = tt % nb;
+    item = src_item = tt / nb;
+  }
+  const int64_t bx = t % bw, by = (t / bw) % bh, bz = t / (bw * bh);
   float f[4] = {filt[0], filt[1], filt[2], filt[3]};  // lo0 lo1 hi0 hi1
   float v[B][B][B];
-  const float* src = in + item * g.D * g.H * g.W + (bz * B * g.H + by * B) * g.W + bx * B;
+  const float* src = in + src_item * g.D * g.H * g.W + (bz * B * g.H + by * B) * g.W + bx * B;
 #pragma unroll
   for (int z = 0; z < B; ++z)
 #pragma unroll
@@ -105,6 +130,25 @@ __global__ void __launch_bounds__(kT3) k_haar3_ana(const float* __restrict__ in,
         v[z][y][1] = q.y;
       }
     }
+  if constexpr (NOISE) {
+    // element group of row (z, y): ((bz B + z) H + by B + y) W / 4 + bx B / 4 (W % 4 == 0, host check)
+    const uint32_t W4 = (uint32_t)(g.W / 4);
+    const uint32_t g0 = (uint32_t)(bz * B * g.H + by * B) * W4 + (uint32_t)(bx * B / 4);
+    const uint32_t img = (uint32_t)(nz.image_base + src_item), sm = (uint32_t)smp;
+#pragma unroll
+    for (int r = 0; r < B * B; r += 2) {
+      const int z0 = r / B, y0 = r % B, z1 = (r + 1) / B, y1 = (r + 1) % B;
+      float za[4], zb[4];
+      wam_normal4_x2(g0 + (uint32_t)(z0 * g.H + y0) * W4, g0 + (uint32_t)(z1 * g.H + y1) * W4, img, sm, nz.k0, nz.k1,
+                     za, zb);
+      const int q = (int)((bx * B) & 3);  // B = 2: the half of the group this block holds
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        v[z0][y0][k] = fmaf(sg, za[q + k], v[z0][y0][k]);  // noisy = fma(sigma, z, x) (wam_noise_add)
+        v[z1][y1][k] = fmaf(sg, zb[q + k], v[z1][y1][k]);
+      }
+    }
+  }
   // level 1 (finest): B/2 x B/2 x B/2 blocks of 2^3
   constexpr int B1 = B / 2;
   float ll[B1][B1][B1];
@@ -262,10 +306,37 @@ int launch_dwt3_haar_analysis(const wam_plan* p, int64_t batch, const float* in,
   if (grid > 0x7fffffff) return WAM_ERR_UNSUPPORTED;
   const float* filt = p->d_filt + (adjoint ? WAM_F_ADJ_LO : WAM_F_ANA_LO) * p->L;  // lo0 lo1 hi0 hi1
   WamTimer tm(st, "k_haar3_ana", 4.0 * (double)batch * ((double)g.D * g.H * g.W + (double)p->band_off[p->nbands]));
+  const WamNoise none{nullptr, 1, 1, 0, 0, 0, 0};
   if (p->levels == 1)
-    hipLaunchKernelGGL(k_haar3_ana<1>, dim3((unsigned)grid), dim3(kT3), 0, st, in, coeffs, filt, g, blocks);
+    hipLaunchKernelGGL((k_haar3_ana<1, false>), dim3((unsigned)grid), dim3(kT3), 0, st, in, coeffs, filt, g, blocks,
+                       none, (int64_t)1);
   else
-    hipLaunchKernelGGL(k_haar3_ana<2>, dim3((unsigned)grid), dim3(kT3), 0, st, in, coeffs, filt, g, blocks);
+    hipLaunchKernelGGL((k_haar3_ana<2, false>), dim3((unsigned)grid), dim3(kT3), 0, st, in, coeffs, filt, g, blocks,
+                       none, (int64_t)1);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int launch_dwt3_haar_analysis_noisy(const wam_plan* p, int64_t batch, const float* in, float* coeffs,
+                                    const WamNoise* nz, int64_t n_samples, hipStream_t st) {
+  if (!dwt3_haar_supported(p) || ((uintptr_t)in & 15) || !nz) return WAM_ERR_UNSUPPORTED;
+  if (nz->channels != 1 || batch != n_samples * nz->images) return WAM_ERR_UNSUPPORTED;
+  const Haar3Geom g = make_geom3(p, batch);
+  if (g.W % 4 || g.D * g.H * g.W >= (int64_t(1) << 34)) return WAM_ERR_UNSUPPORTED;  // 32-bit element groups
+  const int B = 1 << p->levels;
+  const int64_t nb = (g.D / B) * (g.H / B) * (g.W / B);
+  const int64_t grid = n_samples * nz->images * ((nb + kT3 - 1) / kT3);
+  if (grid > 0x7fffffff) return WAM_ERR_UNSUPPORTED;
+  const float* filt = p->d_filt + WAM_F_ANA_LO * p->L;
+  const double vol = (double)g.D * g.H * g.W;
+  // algorithmic bytes: the clean volumes once, every sample's coefficients
+  WamTimer tm(st, "k_haar3_ana<noise>", 4.0 * ((double)nz->images * vol + (double)batch * p->band_off[p->nbands]));
+  if (p->levels == 1)
+    hipLaunchKernelGGL((k_haar3_ana<1, true>), dim3((unsigned)grid), dim3(kT3), 0, st, in, coeffs, filt, g, batch * nb,
+                       *nz, n_samples);
+  else
+    hipLaunchKernelGGL((k_haar3_ana<2, true>), dim3((unsigned)grid), dim3(kT3), 0, st, in, coeffs, filt, g, batch * nb,
+                       *nz, n_samples);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }

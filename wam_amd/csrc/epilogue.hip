@@ -127,10 +127,17 @@ struct BandTable {
 };
 constexpr int kMapTile = 8192;  // elements per block (32 per thread): one band-max atomic per 32 KB
 
-// grid: x = tile (over all bands), y = item. One atomic max per block.
+// grid: x = tile (over all bands), y = item. One atomic max per block. Every thread issues all of
+// its loads of a channel before using any (addresses clamped into the band, results of the clamped
+// slots dropped at the store): a load guarded by `q < nb` made the compiler wait for each one in
+// turn. VEC4 (host check: every band offset and length a multiple of 4): 16-byte loads / stores.
+template <bool VEC4>
 __global__ void __launch_bounds__(256) k_subband_maps(BandTable bt, int64_t items_total, int64_t group_items,
                                                       int channels, const float* __restrict__ g,
                                                       float* __restrict__ maps, float* __restrict__ band_max) {
+  constexpr int PER = kMapTile / 256;  // elements per thread
+  constexpr int V = VEC4 ? 4 : 1;
+  constexpr int NL = PER / V;          // loads per thread and channel
   const int tile = blockIdx.x;
   int b = 0;
   while (b + 1 < bt.nbands && bt.tile0[b + 1] <= tile) ++b;
@@ -139,16 +146,40 @@ __global__ void __launch_bounds__(256) k_subband_maps(BandTable bt, int64_t item
   const int64_t q0 = (int64_t)(tile - bt.tile0[b]) * kMapTile;
   const float* base = g + items_total * channels * bt.off[b] + (item * channels) * nb;
   float* out = maps + item * bt.off[bt.nbands] + bt.off[b];
+  float acc[PER];
+  for (int c = 0; c < channels; ++c) {
+    const float* bc = base + (int64_t)c * nb;
+    float ld[PER];
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+      const int64_t q = q0 + ((int64_t)u * 256 + threadIdx.x) * V;
+      const int64_t qc = q < nb ? q : nb - V;
+      if constexpr (VEC4) {
+        const float4 t = *reinterpret_cast<const float4*>(bc + qc);
+        ld[4 * u] = t.x;
+        ld[4 * u + 1] = t.y;
+        ld[4 * u + 2] = t.z;
+        ld[4 * u + 3] = t.w;
+      } else {
+        ld[u] = bc[qc];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) acc[k] = c ? acc[k] + ld[k] : ld[k];  // ((g0 + g1) + g2): numpy's sum
+  }
+  const float inv_c = (float)channels;
   float m = 0.f;
 #pragma unroll
-  for (int u = 0; u < kMapTile / 256; ++u) {
-    const int64_t q = q0 + u * 256 + threadIdx.x;
+  for (int u = 0; u < NL; ++u) {
+    const int64_t q = q0 + ((int64_t)u * 256 + threadIdx.x) * V;
+    float v[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = fabsf(acc[V * u + k] / inv_c);  // numpy mean: sum then true_divide
     if (q < nb) {
-      float acc = base[q];
-      for (int c = 1; c < channels; ++c) acc = acc + base[(int64_t)c * nb + q];
-      float v = fabsf(acc / (float)channels);  // numpy mean: sum then true_divide
-      out[q] = v;
-      m = nan_max(m, v);
+      if constexpr (VEC4) *reinterpret_cast<float4*>(out + q) = make_float4(v[0], v[1], v[2], v[3]);
+      else out[q] = v[0];
+#pragma unroll
+      for (int k = 0; k < V; ++k) m = nan_max(m, v[k]);
     }
   }
 #pragma unroll
@@ -566,8 +597,14 @@ int wam_subband_maps(const wam_plan* p, int64_t groups, int64_t group_items, int
     if (b < p->nbands) tiles += (int)((p->band_off[b + 1] - p->band_off[b] + kMapTile - 1) / kMapTile);
   }
   WamTimer tm((hipStream_t)stream, "k_subband_maps", 4.0 * (double)items * (channels + 1) * p->band_off[p->nbands]);
-  hipLaunchKernelGGL(k_subband_maps, dim3((unsigned)tiles, (unsigned)items), dim3(256), 0, (hipStream_t)stream, bt,
-                     items, group_items, channels, coeff_grads, maps, band_max);
+  bool vec4 = ((uintptr_t)coeff_grads & 15) == 0 && ((uintptr_t)maps & 15) == 0;
+  for (int b = 0; b <= p->nbands; ++b) vec4 = vec4 && (p->band_off[b] % 4 == 0);
+  if (vec4)
+    hipLaunchKernelGGL(k_subband_maps<true>, dim3((unsigned)tiles, (unsigned)items), dim3(256), 0,
+                       (hipStream_t)stream, bt, items, group_items, channels, coeff_grads, maps, band_max);
+  else
+    hipLaunchKernelGGL(k_subband_maps<false>, dim3((unsigned)tiles, (unsigned)items), dim3(256), 0,
+                       (hipStream_t)stream, bt, items, group_items, channels, coeff_grads, maps, band_max);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }

@@ -70,5 +70,8 @@ int launch_dwt1_tile_synthesis(const wam_plan* p, int64_t batch, const float* co
 bool dwt3_haar_supported(const wam_plan* p);
 int launch_dwt3_haar_analysis(const wam_plan* p, int64_t batch, const float* in, float* coeffs, bool adjoint,
                               hipStream_t st);
+// noise fused on the load (single-channel volumes; wam_wavedec_noisy for 3D Haar plans)
+int launch_dwt3_haar_analysis_noisy(const wam_plan* p, int64_t batch, const float* in, float* coeffs,
+                                    const WamNoise* nz, int64_t n_samples, hipStream_t st);
 int launch_dwt3_haar_synthesis(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha, int n_alpha,
                                float* out, hipStream_t st);

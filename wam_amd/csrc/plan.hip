@@ -355,8 +355,9 @@ int analysis_driver(const wam_plan* p, int64_t batch, const float* x, float* coe
     int rc = launch_dwt1_tile_analysis(p, batch, x, coeffs, adjoint, st);
     if (rc != WAM_ERR_UNSUPPORTED) return rc;
   }
-  if (p->ndim == 3 && !noise && !(p->flags & WAM_PLAN_GENERIC)) {  // Haar: all levels per block
-    int rc = launch_dwt3_haar_analysis(p, batch, x, coeffs, adjoint, st);
+  if (p->ndim == 3 && !(p->flags & WAM_PLAN_GENERIC)) {  // Haar: all levels per block
+    int rc = noise ? launch_dwt3_haar_analysis_noisy(p, batch, x, coeffs, noise, n_samples, st)
+                   : launch_dwt3_haar_analysis(p, batch, x, coeffs, adjoint, st);
     if (rc != WAM_ERR_UNSUPPORTED) return rc;
   }
   int nd = p->ndim;
@@ -414,6 +415,8 @@ int wam_plan_caps(const wam_plan* p) {
   for (int l = 0; l < p->levels; ++l) rows_all = rows_all && use_rows(p, l, true);
   if (rows_all || use_plane(p, true)) caps |= WAM_CAP_ADJOINT_MAPS;
   if (use_plane(p, false) || (use_rows(p, 0, false) && p->lin[0][1] % 4 == 0)) caps |= WAM_CAP_NOISY_WAVEDEC;
+  if (p->ndim == 3 && !(p->flags & WAM_PLAN_GENERIC) && dwt3_haar_supported(p) && p->lin[0][2] % 4 == 0)
+    caps |= WAM_CAP_NOISY_WAVEDEC;  // single-channel volumes (channels != 1: WAM_ERR_UNSUPPORTED)
   return caps;
 }
 

@@ -22,7 +22,7 @@ from .constants import KEYS3
 from .engine import (LegacyNoise, Shard, auto_group, chunks, ig_weights, input_gradient, legacy3d_weights,
                      model_device, require_gpu_device)
 from ._lib import check, lib, ptr, stream_of
-from .plan import cube_accumulate, get_plan, item_sigma, noise_add, subband_maps
+from .plan import CAP_NOISY_WAVEDEC, cube_accumulate, get_plan, item_sigma, noise_add, subband_maps
 
 
 class BaseWAM3D:
@@ -298,8 +298,12 @@ class WaveletAttribution3D(BaseWAM3D):
                     full = torch.zeros((cnt, n, c) + sp, dtype=torch.float32, device=dev)
                     full[:, :, 0] = host
                     host = full
-            noisy = noise_add(x, sigma, cnt, n, c * vol, vol, seed=self.random_seed, sample_base=s0, host_noise=host)
-            flat = plan.wavedec(noisy.view((cnt * n * c,) + sp))
+            if host is None and c == 1 and plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
+                flat = plan.wavedec_noisy(x, sigma, cnt, n, 1, self.random_seed, s0)
+            else:
+                noisy = noise_add(x, sigma, cnt, n, c * vol, vol, seed=self.random_seed, sample_base=s0,
+                                  host_noise=host)
+                flat = plan.wavedec(noisy.view((cnt * n * c,) + sp))
             cg = self._grads(plan, flat, cnt * n * c, y, cnt, n, c)
             if shard.world == 1:
                 self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 0, n_total=float(ns))
