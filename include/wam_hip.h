@@ -108,7 +108,7 @@ int wam_plan_caps(const wam_plan* plan);
  * Philox stream as wam_noise_add (counter (sample_base + s, image, element / 4)), without
  * materialising the noisy input. x: [images, channels, H, W]; coeffs band-major over the
  * (sample, image, channel) planes. WAM_ERR_UNSUPPORTED unless WAM_CAP_NOISY_WAVEDEC. Also 3D Haar
- * plans (J <= 2, dims divisible by 2^J, W % 4 == 0; lib/wam_3D.py:565-575) for channels == 1:
+ * plans (J <= 2, dims divisible by 2^J, W % 4 == 0; lib/wam_3D.py:565-582) for channels == 1:
  * x [images, 1, D, H, W], coeffs over the (sample, image) volumes. */
 int wam_wavedec_noisy(const wam_plan* plan, int64_t n_samples, int64_t images, int channels,
                       const float* x, const float* sigma, uint64_t seed, int64_t sample_base,
