@@ -243,18 +243,28 @@ def kernel_table(records, steps):
     return kern
 
 
-def unit_bytes(wl, kname, units_per_launch):
-    """SURVEY 8(d) algorithmic bytes of one launch where they differ from the library's own count
-    (the fused noisy analysis reads the clean input once for all its samples; 8(d) counts the
-    input of every (image x sample) unit, as the reference materialises each noisy image)."""
+def unit_bytes(wl, kname, units_per_launch, lib_bytes, n_items):
+    """SURVEY 8(d) algorithmic bytes of one launch where they differ from the library's own count:
+    the fused noisy analyses (k_*<noise>) read the clean input once for all their samples, while
+    8(d) counts 4 (P + K) per (item x sample) unit, as the reference materialises each noisy input.
+    A kernel that covers only part of each item (the 1D interior / boundary tiles) keeps its share:
+    the library's bytes over the whole-item library count."""
     from wam_amd import plan as P
-    if wl.name != "c2":
+    if wl.name == "c2" and kname in ("k_plane_syn", "k_plane_maps"):
+        K = P.get_plan(2, (224, 224), 3, "db4", "reflect", "cuda").coeff_numel
+        per_unit = {"k_plane_syn": 4 * 3 * (K + 224 * 224), "k_plane_maps": 4 * (3 * 224 * 224 + K)}[kname]
+        return per_unit * units_per_launch
+    if not kname.endswith("<noise>"):
         return None
-    K = P.get_plan(2, (224, 224), 3, "db4", "reflect", "cuda").coeff_numel
-    per_unit = {"k_plane_ana<noise>": 4 * 3 * (224 * 224 + K),           # analysis 4 (P + K)
-                "k_plane_syn": 4 * 3 * (K + 224 * 224),
-                "k_plane_maps": 4 * (3 * 224 * 224 + K)}.get(kname)
-    return None if per_unit is None else per_unit * units_per_launch
+    geo = {"c1": (2, (224, 224), 3, "haar", "reflect", 3), "c2": (2, (224, 224), 3, "db4", "reflect", 3),
+           "c3": (1, (80000,), 5, "db6", "reflect", 1), "c5": (3, (128, 128, 128), 2, "haar", "symmetric", 1)}
+    if wl.name not in geo:
+        return None
+    nd, shape, J, wav, mode, C = geo[wl.name]
+    K = P.get_plan(nd, shape, J, wav, mode, "cuda").coeff_numel * C  # per item (all channels)
+    Pn = int(np.prod(shape)) * C
+    whole = 4.0 * (n_items * Pn + units_per_launch * K)                # the library's whole-item count
+    return lib_bytes / whole * 4.0 * units_per_launch * (Pn + K)
 
 
 # FFT front-end kernels (wam_amd/csrc/melspec.hip): VALU / LDS bound by construction (two to three
@@ -274,12 +284,12 @@ def traffic_table(kern, traffic):
     return out or None
 
 
-def roofline(wl, kern, steps, units_per_step, traffic):
+def roofline(wl, kern, steps, units_per_step, traffic, n_items):
     hbm = {n: k for n, k in kern.items() if n not in VALU_BOUND} or kern
     dom = max(hbm, key=lambda n: hbm[n]["total_ms"])
     kd = kern[dom]
     units_per_launch = units_per_step * steps / kd["launches"]
-    ub = unit_bytes(wl, dom, units_per_launch)
+    ub = unit_bytes(wl, dom, units_per_launch, kd["bytes_per_launch"], n_items)
     bpl = ub if ub else kd["bytes_per_launch"]
     achieved = bpl / (kd["mean_us"] * 1e-6) / 1e9
     tr = None
@@ -633,7 +643,7 @@ def main():
     assert np.isfinite(np.asarray(first)).all()
     kern = kernel_table(records, args.steps)
     units_per_step = n_local * s_local  # (item x sample) units this rank's launches processed
-    roof = roofline(wl, kern, args.steps, units_per_step, traffic)
+    roof = roofline(wl, kern, args.steps, units_per_step, traffic, n_local)
     if traffic and "error" in traffic:
         roof["traffic_error"] = traffic["error"]
 

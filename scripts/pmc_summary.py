@@ -20,7 +20,7 @@ def short(name):
         return None
     base = m.group(1)
     args = [a.strip() for a in m.group(3).split(",")] if m.group(3) else []
-    if base in ("k_ana_rows", "k_haar3_ana") and args and args[-1] == "true":
+    if base in ("k_ana_rows", "k_haar3_ana", "k_dwt1_ana", "k_dwt1_ana_p", "k_dwt1_ana_int") and args and args[-1] == "true":
         return base + "<noise>"
     if base == "k_plane_ana" and len(args) >= 5:  # <L, CPL, NOISE, MC, MAPS>
         if args[4] == "true":

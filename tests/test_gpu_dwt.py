@@ -227,6 +227,24 @@ def test_noisy_wavedec_equals_noise_then_wavedec(wam, wav, J):
     assert torch.equal(fused, ref)
 
 
+@pytest.mark.parametrize("n,J,wav,mode,S,N", [(80000, 5, "db6", "reflect", 3, 2), (9000, 5, "db6", "constant", 2, 3),
+                                            (4096, 3, "haar", "symmetric", 4, 2), (1000, 4, "sym8", "zero", 2, 2),
+                                            (40, 3, "db4", "reflect", 3, 1), (50000, 4, "coif2", "reflect", 2, 2)])
+def test_noisy_dwt1_equals_noise_then_wavedec(wam, n, J, wav, mode, S, N):
+    """1D tile analysis with the SmoothGrad noise fused on the load -- interior tiles (aligned groups
+    of 4, one Philox call each, samples fastest), persistent and generic boundary tiles (per-sample
+    calls) -- vs wam_noise_add + the same analysis: bit-identical, with a sample base and a seed."""
+    p = wam.get_plan(1, (n,), J, wav, mode, "cuda")
+    assert p.caps & wam.CAP_NOISY_WAVEDEC
+    torch.manual_seed(13)
+    x = torch.randn(N, n, device="cuda")
+    sigma = wam.item_sigma(x, n, n, 0.2)
+    fused = p.wavedec_noisy(x, sigma, S, N, 1, seed=91, sample_base=5)
+    noisy = wam.noise_add(x, sigma, S, N, n, n, seed=91, sample_base=5)
+    ref = p.wavedec(noisy.view(S * N, n))
+    assert torch.equal(fused, ref)
+
+
 @pytest.mark.parametrize("shape,J,mode,S,N", [((128, 128, 128), 2, "symmetric", 2, 3), ((16, 12, 20), 1, "reflect", 3, 2),
                                               ((8, 16, 24), 2, "zero", 5, 1), ((6, 10, 4), 1, "symmetric", 2, 4)])
 def test_noisy_haar3_equals_noise_then_wavedec(wam, shape, J, mode, S, N):

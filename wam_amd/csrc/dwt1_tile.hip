@@ -19,6 +19,7 @@
 #include <type_traits>
 
 #include "kernels.hpp"
+#include "rng.hpp"
 
 namespace {
 
@@ -72,6 +73,26 @@ __device__ __forceinline__ int ext_near(int i, int n, int mode) {
     default: r = i < 0 ? -i - 1 : 2 * n - 1 - i; break;  // symmetric
   }
   return (r >= 0 && r < n) ? r : wam_ext_index(i, n, mode);
+}
+
+// SmoothGrad noise of source sample si of one signal (the wam_noise_add stream: one Philox call per
+// group of 4 samples; here a call per sample -- the boundary tiles only)
+__device__ __forceinline__ float noise_at(int64_t si, uint32_t img, uint32_t smp, uint32_t k0, uint32_t k1) {
+  float z[4];
+  wam_normal4(si >> 2, img, smp, k0, k1, z);
+  const int q = (int)(si & 3);
+  return q == 0 ? z[0] : q == 1 ? z[1] : q == 2 ? z[2] : z[3];
+}
+
+// NOISE: output item `item` (sample-major: s * images + i) is signal i noised for sample s
+struct NoiseItem {
+  int64_t src;   // clean signal index
+  uint32_t img, smp;
+  float sg;
+};
+__device__ __forceinline__ NoiseItem noise_item(const WamNoise& nz, int64_t item) {
+  const int64_t s = item / nz.images, i = item - s * nz.images;
+  return {i, (uint32_t)(nz.image_base + i), (uint32_t)(nz.sample_base + s), nz.sigma[i]};
 }
 
 // ranges (uniform): own [s, e) and computed [S, E) of every level for tile `tile`
@@ -183,9 +204,10 @@ __device__ __forceinline__ void ana_tile_levels(float* smem, const float* flo, c
 }
 
 // tiles [t_lo, t_hi) are left to k_dwt1_ana_int; this kernel runs the others (nb per signal)
-template <int L>
+template <int L, bool NOISE>
 __global__ void __launch_bounds__(kT1) k_dwt1_ana(const float* __restrict__ in, float* __restrict__ coeffs,
-                                                 const float* __restrict__ filt, Dwt1Geom g, int t_lo, int t_hi) {
+                                                 const float* __restrict__ filt, Dwt1Geom g, int t_lo, int t_hi,
+                                                 WamNoise nz) {
   constexpr int p = L - 2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
@@ -205,10 +227,15 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana(const float* __restrict__ in, 
   // window = extended indices [2 S0 - p, 2 E0 - 1) of the input
   const int w0 = 2 * S[0] - p;
   const int wlen = 2 * (E[0] - S[0]) + L - 2;
-  const float* x = in + item * (int64_t)g.n;
+  NoiseItem ni{item, 0, 0, 0.f};
+  if constexpr (NOISE) ni = noise_item(nz, item);
+  const float* x = in + ni.src * (int64_t)g.n;
   for (int j = tid; j < wlen; j += kT1) {
     const int si = ext_near(w0 + j, g.n, g.mode);
-    smem[j] = si >= 0 ? x[si] : 0.f;
+    float v = si >= 0 ? x[si] : 0.f;
+    if constexpr (NOISE)
+      if (si >= 0) v = fmaf(ni.sg, noise_at(si, ni.img, ni.smp, nz.k0, nz.k1), v);  // wam_noise_add's rounding
+    smem[j] = v;
   }
   __syncthreads();
   ana_tile_levels<L>(smem, flo, fhi, g, coeffs, item, S, E, s, e);
@@ -219,10 +246,10 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana(const float* __restrict__ in, 
 // used when every boundary window fits kPF floats per thread
 constexpr int kPF = 20;  // window floats prefetched per thread (window <= kPF * kT1)
 
-template <int L>
+template <int L, bool NOISE>
 __global__ void __launch_bounds__(kT1) k_dwt1_ana_p(const float* __restrict__ in, float* __restrict__ coeffs,
                                                    const float* __restrict__ filt, Dwt1Geom g, int t_lo, int t_hi,
-                                                   int64_t units) {
+                                                   int64_t units, WamNoise nz) {
   constexpr int p = L - 2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
@@ -242,7 +269,7 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_p(const float* __restrict__ in
   uint32_t zmask = 0;  // window slots that are zeros (zero-mode extension): applied when stored, so
                        // the loads themselves stay unconditional and all in flight together
   auto prefetch = [&](int64_t u, int slot) {
-    const int64_t item = u / nb;
+    const int64_t item = NOISE ? noise_item(nz, u / nb).src : u / nb;
     const int w0 = 2 * R[slot][0][0] - p;
     const int wlen = 2 * (R[slot][1][0] - R[slot][0][0]) + L - 2;
     const float* x = in + item * (int64_t)g.n;
@@ -264,10 +291,19 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_p(const float* __restrict__ in
   }
   for (; u < units; u += gridDim.x) {
     const int wlen = 2 * (R[cur][1][0] - R[cur][0][0]) + L - 2;
+    NoiseItem ni{0, 0, 0, 0.f};
+    if constexpr (NOISE) ni = noise_item(nz, u / nb);
 #pragma unroll
     for (int r = 0; r < kPF; ++r) {
       const int j = tid + r * kT1;
-      if (j < wlen) smem[j] = (zmask >> r) & 1u ? 0.f : pf[r];
+      if (j < wlen) {
+        float v = (zmask >> r) & 1u ? 0.f : pf[r];
+        if constexpr (NOISE)
+          if (!((zmask >> r) & 1u))  // the window sample's source index (the extension applied)
+            v = fmaf(ni.sg, noise_at(ext_near(2 * R[cur][0][0] - p + j, g.n, g.mode), ni.img, ni.smp, nz.k0, nz.k1),
+                     v);
+        smem[j] = v;
+      }
     }
     const int64_t un = u + gridDim.x;
     if (tid == 0 && un < units) ranges(un, cur ^ 1);
@@ -289,10 +325,16 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_p(const float* __restrict__ in
 
 __host__ __device__ __forceinline__ int eo_cap(int n) { return (((n + 1) / 2 + 31) & ~31) + 16; }
 
-template <int L>
+// NOISE: the window is fetched as aligned groups of 4 samples (float4; the signal length is a
+// multiple of 4, host check), each noised with ONE Philox call of wam_noise_add's stream (two
+// groups per interleaved call pair); units run sample-fastest over XCD-swizzled workgroups, so
+// the S samples of a (signal, tile) read its window from one L2.
+constexpr int kPG = 6;  // noisy window: float4 groups per thread (window <= (kPG * kT1 - 1) * 4)
+
+template <int L, bool NOISE>
 __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ in, float* __restrict__ coeffs,
                                                      const float* __restrict__ filt, Dwt1Geom g, int t_lo, int t_hi,
-                                                     int64_t units) {
+                                                     int64_t units, WamNoise nz, int64_t S) {
   constexpr int p = L - 2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
@@ -313,34 +355,77 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ 
   float* winO = smem + cw;
   const int c1 = eo_cap((n0 - p) >> 1);
   float* bufA = smem + 2 * cw;            // even levels' outputs (level 0: n0 values)
-  float* bufB = bufA + 2 * c0;            // odd levels' outputs (level 1: (n0 - p) / 2 values)
-  auto unit_geom = [&](int64_t u, int64_t& item, int& tile, int& S0) {
-    item = u / nti;
-    tile = t_lo + (int)(u - item * nti);
+  float* bufB = smem;                     // odd levels' outputs, in the window's space (dead after level 0)
+  // unit -> output item and tile; NOISE: sample fastest, src = the clean signal
+  auto unit_geom = [&](int64_t u, int64_t& item, int64_t& src, int& tile, int& S0) {
+    if constexpr (NOISE) {
+      const int64_t s = u % S, rest = u / S, i = rest / nti;
+      tile = t_lo + (int)(rest - i * nti);
+      src = i;
+      item = s * nz.images + i;
+    } else {
+      item = src = u / nti;
+      tile = t_lo + (int)(u - item * nti);
+    }
     S0 = ((tile * tj) << (J - 1)) - p * ((1 << (J - 1)) - 1);
   };
-  float pf[kPF];
+  constexpr int NPF = NOISE ? 4 * kPG : kPF;
+  float pf[NPF];
   auto prefetch = [&](int64_t u) {
-    int64_t item;
+    int64_t item, src;
     int tile, S0;
-    unit_geom(u < units ? u : units - 1, item, tile, S0);
-    const float* x = in + item * (int64_t)g.n + (2 * S0 - p);
+    unit_geom(u < units ? u : units - 1, item, src, tile, S0);
+    if constexpr (NOISE) {
+      // aligned groups [ga, gb) covering the window [w0, w0 + wlen); clamped to the last one
+      const int w0 = 2 * S0 - p, ga = w0 >> 2, gb = (w0 + wlen + 3) >> 2;
+      const float4* x4 = reinterpret_cast<const float4*>(in + src * (int64_t)g.n);
 #pragma unroll
-    for (int r = 0; r < kPF; ++r) {
-      const int j = tid + r * kT1;
-      pf[r] = x[j < wlen ? j : wlen - 1];
+      for (int r = 0; r < kPG; ++r) {
+        const int gi = ga + tid + r * kT1;
+        const float4 t = x4[gi < gb ? gi : gb - 1];
+        pf[4 * r] = t.x;
+        pf[4 * r + 1] = t.y;
+        pf[4 * r + 2] = t.z;
+        pf[4 * r + 3] = t.w;
+      }
+    } else {
+      const float* x = in + src * (int64_t)g.n + (2 * S0 - p);
+#pragma unroll
+      for (int r = 0; r < kPF; ++r) {
+        const int j = tid + r * kT1;
+        pf[r] = x[j < wlen ? j : wlen - 1];
+      }
     }
   };
-  int64_t u = blockIdx.x;
+  int64_t u = NOISE ? wam_xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
   if (u < units) prefetch(u);
   for (; u < units; u += gridDim.x) {
-    int64_t item;
+    int64_t item, src;
     int tile, S0;
-    unit_geom(u, item, tile, S0);
+    unit_geom(u, item, src, tile, S0);
+    if constexpr (NOISE) {
+      const NoiseItem ni = noise_item(nz, item);
+      const int w0 = 2 * S0 - p, ga = w0 >> 2, gb = (w0 + wlen + 3) >> 2;
 #pragma unroll
-    for (int r = 0; r < kPF; ++r) {
-      const int j = tid + r * kT1;
-      if (j < wlen) ((j & 1) ? winO : winE)[j >> 1] = pf[r];
+      for (int r = 0; r < kPG; r += 2) {
+        const int gi0 = ga + tid + r * kT1, gi1 = gi0 + kT1;
+        float za[4], zb[4];
+        wam_normal4_x2((uint32_t)gi0, (uint32_t)gi1, ni.img, ni.smp, nz.k0, nz.k1, za, zb);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int ja = 4 * gi0 + k - w0, jb = 4 * gi1 + k - w0;
+          if (gi0 < gb && ja >= 0 && ja < wlen)
+            ((ja & 1) ? winO : winE)[ja >> 1] = fmaf(ni.sg, za[k], pf[4 * r + k]);  // wam_noise_add's rounding
+          if (gi1 < gb && jb >= 0 && jb < wlen)
+            ((jb & 1) ? winO : winE)[jb >> 1] = fmaf(ni.sg, zb[k], pf[4 * (r + 1) + k]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < kPF; ++r) {
+        const int j = tid + r * kT1;
+        if (j < wlen) ((j & 1) ? winO : winE)[j >> 1] = pf[r];
+      }
     }
     __syncthreads();
     prefetch(u + gridDim.x);  // in flight while the levels run
@@ -702,9 +787,12 @@ void interior_range(const Dwt1Geom& g, int p, int& t_lo, int& t_hi) {
   if (t_hi <= t_lo) t_lo = t_hi = 0;
 }
 
+// window (E / O) + the even levels' buffer; the odd levels reuse the window's space: 51.5 KB at
+// c3's 4,096-sample tiles, so three workgroups fit a CU (the noisy kernel's 57 VGPRs allow six
+// waves per SIMD)
 int ana_int_lds_bytes(const Dwt1Geom& g, int p) {
   const int n0 = (g.tile_j << (g.J - 1)) + p * ((1 << (g.J - 1)) - 1);
-  return (2 * eo_cap(2 * n0 + p) + 2 * eo_cap(n0) + 2 * eo_cap((n0 - p) >> 1)) * 4;
+  return (2 * eo_cap(2 * n0 + p) + 2 * eo_cap(n0)) * 4;
 }
 
 int syn_lds_bytes(const wam_plan* p) {
@@ -724,8 +812,16 @@ bool dwt1_tile_supported(const wam_plan* p, bool adjoint) {
 }
 
 int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in, float* coeffs, bool adjoint,
-                              hipStream_t st) {
+                              hipStream_t st, const WamNoise* nz, int64_t n_samples) {
   if (!dwt1_tile_supported(p, adjoint)) return WAM_ERR_UNSUPPORTED;
+  if (nz) {  // SmoothGrad noise fused on the load: single-channel signals, length a multiple of 4
+    if (adjoint || nz->channels != 1 || batch != n_samples * nz->images || p->lin[0][0] % 4 ||
+        ((uintptr_t)in & 15))
+      return WAM_ERR_UNSUPPORTED;
+  }
+  const WamNoise none{nullptr, 1, 1, 0, 0, 0, 0};
+  const WamNoise& NZ = nz ? *nz : none;
+  const int64_t S = nz ? n_samples : 1;
   const int n = (int)(adjoint ? p->rec_shape[0] : p->lin[0][0]);
   const int mode = adjoint ? WAM_MODE_ZERO : p->mode;
   const Dwt1Geom g = make_geom1(p, n, mode, batch);
@@ -741,25 +837,41 @@ int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in,
   if (2 * n0 + pp > kPF * kT1 || lds_i > kLds1Cap) t_lo = t_hi = 0;  // window too long: all tiles generic
   const int64_t units = batch * (int64_t)(t_hi - t_lo);
   const int64_t nb_blocks = batch * (int64_t)(g.tiles - (t_hi - t_lo));
-  const double bytes = 4.0 * (double)batch * ((double)n + (double)p->band_off[p->nbands]);
+  // algorithmic bytes: every input once (noisy: the clean signals once for all samples) and
+  // every output once
+  const double bytes = nz ? 4.0 * ((double)nz->images * n + (double)batch * p->band_off[p->nbands])
+                          : 4.0 * (double)batch * ((double)n + (double)p->band_off[p->nbands]);
   if (units > 0) {
-    // persistent grid: two 512-thread workgroups per CU (LDS ~60 KB each)
     int dev = 0;
     WAM_HIP_CHECK(hipGetDevice(&dev));
     int cus = 256;
     WAM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const int64_t grid = std::min<int64_t>(units, (int64_t)kAnaWgs * cus);
-    WamTimer tm(st, "k_dwt1_ana_int", bytes * (double)(t_hi - t_lo) / g.tiles);
+    WamTimer tm(st, nz ? "k_dwt1_ana_int<noise>" : "k_dwt1_ana_int", bytes * (double)(t_hi - t_lo) / g.tiles);
+    // persistent grid: exactly the resident workgroups (VGPRs and LDS decide: 2 per CU for the
+    // clean kernel's 107 VGPRs, 3 for the noisy one's 57 at c3's 51.5 KB of LDS), so no workgroup
+    // waits for a slot and the units split evenly
     switch (p->L) {
+#define WAM_D1AIN(LL, NN)                                                                                         \
+  {                                                                                                               \
+    if (int rc = lds_opt_in((const void*)k_dwt1_ana_int<LL, NN>, lds_i)) return rc;                              \
+    int wgs = kAnaWgs;                                                                                            \
+    WAM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, k_dwt1_ana_int<LL, NN>, kT1, lds_i));         \
+    const int64_t grid = std::min<int64_t>(units, (int64_t)std::max(1, wgs) * cus);                              \
+    hipLaunchKernelGGL((k_dwt1_ana_int<LL, NN>), dim3((unsigned)grid), dim3(kT1), lds_i, st, in, coeffs, filt, g, \
+                       t_lo, t_hi, units, NZ, S);                                                                 \
+  }
 #define WAM_D1AI(LL)                                                                                            \
   case LL:                                                                                                      \
-    if (int rc = lds_opt_in((const void*)k_dwt1_ana_int<LL>, lds_i)) return rc;                                \
-    hipLaunchKernelGGL(k_dwt1_ana_int<LL>, dim3((unsigned)grid), dim3(kT1), lds_i, st, in, coeffs, filt, g, t_lo, \
-                       t_hi, units);                                                                            \
+    if (nz) {                                                                                                   \
+      WAM_D1AIN(LL, true)                                                                                       \
+    } else {                                                                                                    \
+      WAM_D1AIN(LL, false)                                                                                      \
+    }                                                                                                           \
     break;
       WAM_D1AI(2) WAM_D1AI(4) WAM_D1AI(6) WAM_D1AI(8) WAM_D1AI(10) WAM_D1AI(12) WAM_D1AI(14) WAM_D1AI(16)
       WAM_D1AI(18) WAM_D1AI(20)
 #undef WAM_D1AI
+#undef WAM_D1AIN
       default: return WAM_ERR_UNSUPPORTED;
     }
     WAM_LAUNCH_CHECK();
@@ -778,32 +890,46 @@ int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in,
     int cus = 256;
     WAM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const int64_t grid = std::min<int64_t>(nb_blocks, (int64_t)kAnaWgs * cus);
-    WamTimer tm(st, "k_dwt1_ana_p", bytes * (double)(g.tiles - (t_hi - t_lo)) / g.tiles);
+    WamTimer tm(st, nz ? "k_dwt1_ana_p<noise>" : "k_dwt1_ana_p", bytes * (double)(g.tiles - (t_hi - t_lo)) / g.tiles);
     switch (p->L) {
+#define WAM_D1APN(LL, NN)                                                                                      \
+  if (int rc = lds_opt_in((const void*)k_dwt1_ana_p<LL, NN>, lds)) return rc;                                 \
+  hipLaunchKernelGGL((k_dwt1_ana_p<LL, NN>), dim3((unsigned)grid), dim3(kT1), lds, st, in, coeffs, filt, g, t_lo, \
+                     t_hi, nb_blocks, NZ);
 #define WAM_D1AP(LL)                                                                                           \
   case LL:                                                                                                     \
-    if (int rc = lds_opt_in((const void*)k_dwt1_ana_p<LL>, lds)) return rc;                                    \
-    hipLaunchKernelGGL(k_dwt1_ana_p<LL>, dim3((unsigned)grid), dim3(kT1), lds, st, in, coeffs, filt, g, t_lo, t_hi, \
-                       nb_blocks);                                                                             \
+    if (nz) {                                                                                                  \
+      WAM_D1APN(LL, true)                                                                                      \
+    } else {                                                                                                   \
+      WAM_D1APN(LL, false)                                                                                     \
+    }                                                                                                          \
     break;
       WAM_D1AP(2) WAM_D1AP(4) WAM_D1AP(6) WAM_D1AP(8) WAM_D1AP(10) WAM_D1AP(12) WAM_D1AP(14) WAM_D1AP(16)
       WAM_D1AP(18) WAM_D1AP(20)
 #undef WAM_D1AP
+#undef WAM_D1APN
       default: return WAM_ERR_UNSUPPORTED;
     }
     WAM_LAUNCH_CHECK();
   } else if (nb_blocks > 0) {
-    WamTimer tm(st, "k_dwt1_ana", bytes * (double)(g.tiles - (t_hi - t_lo)) / g.tiles);
+    WamTimer tm(st, nz ? "k_dwt1_ana<noise>" : "k_dwt1_ana", bytes * (double)(g.tiles - (t_hi - t_lo)) / g.tiles);
     switch (p->L) {
+#define WAM_D1AN(LL, NN)                                                                                     \
+  if (int rc = lds_opt_in((const void*)k_dwt1_ana<LL, NN>, lds)) return rc;                                 \
+  hipLaunchKernelGGL((k_dwt1_ana<LL, NN>), dim3((unsigned)nb_blocks), dim3(kT1), lds, st, in, coeffs, filt, g, \
+                     t_lo, t_hi, NZ);
 #define WAM_D1A(LL)                                                                                          \
   case LL:                                                                                                   \
-    if (int rc = lds_opt_in((const void*)k_dwt1_ana<LL>, lds)) return rc;                                    \
-    hipLaunchKernelGGL(k_dwt1_ana<LL>, dim3((unsigned)nb_blocks), dim3(kT1), lds, st, in, coeffs, filt, g, t_lo, \
-                       t_hi);                                                                                \
+    if (nz) {                                                                                                \
+      WAM_D1AN(LL, true)                                                                                     \
+    } else {                                                                                                 \
+      WAM_D1AN(LL, false)                                                                                    \
+    }                                                                                                        \
     break;
       WAM_D1A(2) WAM_D1A(4) WAM_D1A(6) WAM_D1A(8) WAM_D1A(10) WAM_D1A(12) WAM_D1A(14) WAM_D1A(16) WAM_D1A(18)
       WAM_D1A(20)
 #undef WAM_D1A
+#undef WAM_D1AN
       default: return WAM_ERR_UNSUPPORTED;
     }
     WAM_LAUNCH_CHECK();

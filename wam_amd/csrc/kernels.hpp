@@ -61,8 +61,7 @@ int launch_dwt2_plane_synthesis(const wam_plan* p, int64_t batch, const float* c
 
 // fused multi-level 1D tiles (dwt1_tile.hip)
 bool dwt1_tile_supported(const wam_plan* p, bool adjoint);
-int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in, float* coeffs, bool adjoint,
-                              hipStream_t st);
+
 int launch_dwt1_tile_synthesis(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha,
                                int n_alpha, float* out, hipStream_t st);
 
@@ -70,6 +69,10 @@ int launch_dwt1_tile_synthesis(const wam_plan* p, int64_t batch, const float* co
 bool dwt3_haar_supported(const wam_plan* p);
 int launch_dwt3_haar_analysis(const wam_plan* p, int64_t batch, const float* in, float* coeffs, bool adjoint,
                               hipStream_t st);
+// 1D tiles (dwt1_tile.hip); nz: SmoothGrad noise fused on the load (single-channel signals whose
+// length is a multiple of 4; batch = n_samples x images, sample-major)
+int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in, float* coeffs, bool adjoint,
+                              hipStream_t st, const WamNoise* nz = nullptr, int64_t n_samples = 1);
 // noise fused on the load (single-channel volumes; wam_wavedec_noisy for 3D Haar plans)
 int launch_dwt3_haar_analysis_noisy(const wam_plan* p, int64_t batch, const float* in, float* coeffs,
                                     const WamNoise* nz, int64_t n_samples, hipStream_t st);

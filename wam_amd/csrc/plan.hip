@@ -351,8 +351,8 @@ int analysis_driver(const wam_plan* p, int64_t batch, const float* x, float* coe
     int rc = launch_dwt2_plane_analysis(p, batch, x, coeffs, adjoint, noise, n_samples, st);
     if (rc != WAM_ERR_UNSUPPORTED) return rc;
   }
-  if (p->ndim == 1 && !noise && !(p->flags & WAM_PLAN_GENERIC)) {  // all levels per signal tile
-    int rc = launch_dwt1_tile_analysis(p, batch, x, coeffs, adjoint, st);
+  if (p->ndim == 1 && !(p->flags & WAM_PLAN_GENERIC)) {  // all levels per signal tile
+    int rc = launch_dwt1_tile_analysis(p, batch, x, coeffs, adjoint, st, noise, n_samples);
     if (rc != WAM_ERR_UNSUPPORTED) return rc;
   }
   if (p->ndim == 3 && !(p->flags & WAM_PLAN_GENERIC)) {  // Haar: all levels per block
@@ -415,6 +415,8 @@ int wam_plan_caps(const wam_plan* p) {
   for (int l = 0; l < p->levels; ++l) rows_all = rows_all && use_rows(p, l, true);
   if (rows_all || use_plane(p, true)) caps |= WAM_CAP_ADJOINT_MAPS;
   if (use_plane(p, false) || (use_rows(p, 0, false) && p->lin[0][1] % 4 == 0)) caps |= WAM_CAP_NOISY_WAVEDEC;
+  if (p->ndim == 1 && !(p->flags & WAM_PLAN_GENERIC) && dwt1_tile_supported(p, false) && p->lin[0][0] % 4 == 0)
+    caps |= WAM_CAP_NOISY_WAVEDEC;  // single-channel signals (channels != 1: WAM_ERR_UNSUPPORTED)
   if (p->ndim == 3 && !(p->flags & WAM_PLAN_GENERIC) && dwt3_haar_supported(p) && p->lin[0][2] % 4 == 0)
     caps |= WAM_CAP_NOISY_WAVEDEC;  // single-channel volumes (channels != 1: WAM_ERR_UNSUPPORTED)
   return caps;

@@ -14,7 +14,7 @@ import torch
 from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, LegacyNoise, model_device,
                      require_gpu_device)
 from .melspec import kernel_supported, mel_adjoint, mel_forward, melspec_db
-from .plan import accumulate_f32, get_plan, item_sigma, noise_add, trapz_stream
+from .plan import CAP_NOISY_WAVEDEC, accumulate_f32, get_plan, item_sigma, noise_add, trapz_stream
 
 
 def _peak_normalise(x):
@@ -191,9 +191,12 @@ class WaveletAttribution1D(BaseWAM1D):
         mel_acc = torch.zeros(int(np.prod(self._mel_shape)), dtype=torch.float32, device=dev)
         c_acc = torch.zeros(n * plan.coeff_numel, dtype=torch.float32, device=dev)
         for s0, cnt in chunks(s_lo, s_hi, group):
-            host = None if legacy is None else legacy.chunk(s0, cnt)
-            noisy = noise_add(x, sigma, cnt, n, w, w, seed=self.random_seed, sample_base=s0, host_noise=host)
-            flat = plan.wavedec(noisy.view(cnt * n, w))
+            if legacy is None and plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
+                flat = plan.wavedec_noisy(x, sigma, cnt, n, 1, self.random_seed, s0)
+            else:
+                host = None if legacy is None else legacy.chunk(s0, cnt)
+                noisy = noise_add(x, sigma, cnt, n, w, w, seed=self.random_seed, sample_base=s0, host_noise=host)
+                flat = plan.wavedec(noisy.view(cnt * n, w))
             g_mel, cg = self._grads(plan, flat, cnt * n, y, cnt, n)
             if g_mel.numel() != cnt * mel_acc.numel():
                 raise RuntimeError("melspec gradient shape %s does not match %s" % (tuple(g_mel.shape),
