@@ -265,9 +265,15 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_p(const float* __restrict__ in
     const int kb = (int)(u % nb);
     ana_ranges(g, kb < t_lo ? kb : t_hi + (kb - t_lo), p, R[slot][0], R[slot][1], R[slot][2], R[slot][3]);
   };
-  float pf[kPF];
-  uint32_t zmask = 0;  // window slots that are zeros (zero-mode extension): applied when stored, so
-                       // the loads themselves stay unconditional and all in flight together
+  // NOISE: a thread takes runs of 4 consecutive window samples whose first source index is a
+  // multiple of 4 (window offset shifted by w0 mod 4), so one Philox call (the group of wam_noise_add's
+  // stream) serves the whole run away from the extension's turning points
+  constexpr int kNG = kPF / 4 + 1;
+  constexpr int kPFN = NOISE ? 4 * kNG : kPF;
+  float pf[kPFN];
+  uint32_t zmask = 0;  // window slots that are zeros (zero-mode extension, or outside the window):
+                       // applied when stored, so the loads stay unconditional and all in flight together
+  auto slot_j = [&](int r, int a) { return NOISE ? 4 * (tid + (r >> 2) * kT1) - a + (r & 3) : tid + r * kT1; };
   auto prefetch = [&](int64_t u, int slot) {
     const int64_t item = NOISE ? noise_item(nz, u / nb).src : u / nb;
     const int w0 = 2 * R[slot][0][0] - p;
@@ -275,9 +281,9 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_p(const float* __restrict__ in
     const float* x = in + item * (int64_t)g.n;
     zmask = 0;
 #pragma unroll
-    for (int r = 0; r < kPF; ++r) {
-      const int j = tid + r * kT1;
-      const int si = j < wlen ? ext_near(w0 + j, g.n, g.mode) : -1;
+    for (int r = 0; r < kPFN; ++r) {
+      const int j = slot_j(r, w0 & 3);
+      const int si = (j >= 0 && j < wlen) ? ext_near(w0 + j, g.n, g.mode) : -1;
       zmask |= (si < 0 ? 1u : 0u) << r;
       pf[r] = x[si >= 0 ? si : 0];
     }
@@ -291,18 +297,50 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_p(const float* __restrict__ in
   }
   for (; u < units; u += gridDim.x) {
     const int wlen = 2 * (R[cur][1][0] - R[cur][0][0]) + L - 2;
-    NoiseItem ni{0, 0, 0, 0.f};
-    if constexpr (NOISE) ni = noise_item(nz, u / nb);
+    if constexpr (NOISE) {
+      const NoiseItem ni = noise_item(nz, u / nb);
+      const int w0 = 2 * R[cur][0][0] - p;
 #pragma unroll
-    for (int r = 0; r < kPF; ++r) {
-      const int j = tid + r * kT1;
-      if (j < wlen) {
-        float v = (zmask >> r) & 1u ? 0.f : pf[r];
-        if constexpr (NOISE)
-          if (!((zmask >> r) & 1u))  // the window sample's source index (the extension applied)
-            v = fmaf(ni.sg, noise_at(ext_near(2 * R[cur][0][0] - p + j, g.n, g.mode), ni.img, ni.smp, nz.k0, nz.k1),
-                     v);
-        smem[j] = v;
+      for (int q = 0; q < kNG; ++q) {
+        const int jb = slot_j(4 * q, w0 & 3);
+        if (jb >= wlen) continue;
+        int si[4];
+        int sf = -1, sl = -1;  // first / last source index of the run
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          si[k] = (zmask >> (4 * q + k)) & 1u ? -1 : ext_near(w0 + jb + k, g.n, g.mode);
+          if (si[k] >= 0) {
+            sf = sf < 0 ? si[k] : sf;
+            sl = si[k];
+          }
+        }
+        float za[4] = {0.f, 0.f, 0.f, 0.f}, zb[4] = {0.f, 0.f, 0.f, 0.f};
+        if (sf >= 0) wam_normal4(sf >> 2, ni.img, ni.smp, nz.k0, nz.k1, za);
+        if (sl >= 0 && (sl >> 2) != (sf >> 2)) wam_normal4(sl >> 2, ni.img, ni.smp, nz.k0, nz.k1, zb);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int j = jb + k;
+          if (j < 0 || j >= wlen) continue;
+          float v = 0.f;
+          if (si[k] >= 0) {
+            const int c = si[k] & 3;
+            float z;
+            if ((si[k] >> 2) == (sf >> 2))
+              z = c == 0 ? za[0] : c == 1 ? za[1] : c == 2 ? za[2] : za[3];
+            else if ((si[k] >> 2) == (sl >> 2))
+              z = c == 0 ? zb[0] : c == 1 ? zb[1] : c == 2 ? zb[2] : zb[3];
+            else  // a third group (a turning point inside the run)
+              z = noise_at(si[k], ni.img, ni.smp, nz.k0, nz.k1);
+            v = fmaf(ni.sg, z, pf[4 * q + k]);  // wam_noise_add's rounding
+          }
+          smem[j] = v;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < kPF; ++r) {
+        const int j = tid + r * kT1;
+        if (j < wlen) smem[j] = (zmask >> r) & 1u ? 0.f : pf[r];
       }
     }
     const int64_t un = u + gridDim.x;
