@@ -3,6 +3,7 @@
 usage: python scripts/kbench_nd.py [--iters 5]
 c3: 1D db6 J=5, 256 clips x 80000 samples x 25 noise samples per launch group (6400 signals)
 c5: 3D haar J=2 symmetric, 16 volumes of 128^3 x 25 samples (400 volumes)
+c4: 2D sym8 J=5 reflect at 512^2, 128 images x 3 channels x 2 IG steps per call (768 planes)
 """
 import argparse
 import os
@@ -19,11 +20,12 @@ from wam_amd import plan as P  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--only", default=None, help="c3 or c5")
+    ap.add_argument("--only", default=None, help="c3, c4 or c5")
     args = ap.parse_args()
     torch.manual_seed(0)
     for tag, dim, shape, J, wav, mode, B in [("c3 1D", 1, (80000,), 5, "db6", "reflect", 6400),
-                                             ("c5 3D", 3, (128, 128, 128), 2, "haar", "symmetric", 400)]:
+                                             ("c5 3D", 3, (128, 128, 128), 2, "haar", "symmetric", 400),
+                                             ("c4 2D", 2, (512, 512), 5, "sym8", "reflect", 768)]:
         if args.only and not tag.startswith(args.only):
             continue
         p = P.get_plan(dim, shape, J, wav, mode, "cuda")
