@@ -17,12 +17,11 @@ __device__ __forceinline__ void wsync() { __builtin_amdgcn_wave_barrier(); }
 
 __device__ __forceinline__ float nan_max(float a, float b) { return (a != a || a > b) ? a : b; }
 
-__device__ __attribute__((noinline)) int ext_slow(int i, int n, int mode) { return wam_ext_index(i, n, mode); }
-
-// source row of extended row er (-1 = zero row), fast path for the interior
-__device__ __forceinline__ int row_src(int er, int n, int mode) {
-  return (er >= 0 && er < n) ? er : ext_slow(er, n, mode);
-}
+// source row of extended row er (-1 = zero row). Inlined on purpose: an out-of-line call for the
+// rare far rows in the row loops forced the call ABI's register split on the whole loop (VGPR
+// spills whose scratch reloads drain the row fetches in flight): the noisy plane analysis ran 4 %
+// and the c4 row kernels 3-4 % faster without it (r02h A/B)
+__device__ __forceinline__ int row_src(int er, int n, int mode) { return wam_ext_index(er, n, mode); }
 
 // One source row in registers: VEC-wide loads, MAXV per lane.
 template <int VEC, int MAXV>

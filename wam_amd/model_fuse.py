@@ -138,9 +138,12 @@ def _conv_grad_input(g, x, w, stride, padding, dilation, groups):
 # ConvBiasReLU is a single kernel. Measured on MI355X at the c2 shapes (batch 832, bf16;
 # scripts/gemm_probe.py, profiles/r01g_gemm_probe.log): 1.2-3.2x faster than the MIOpen
 # convolution + epilogue pass forward, 1.1-1.9x faster for the input gradient.
+# bf16 only: fp32 models keep the MIOpen convolutions, because the fp32 GEMM solution hipBLASLt
+# picks varies by box in accumulation precision (one MI355X box gave a 3.4e-3 median relative
+# input-gradient error on ResNet-50 NHWC against 1e-6 for the convolution path, r02h).
 def _pointwise(w, geom):
     stride, padding, dilation, groups = geom
-    return (w.dim() == 4 and w.shape[2] == 1 and w.shape[3] == 1 and groups == 1 and list(stride) == [1, 1]
+    return (w.dtype == torch.bfloat16 and w.dim() == 4 and w.shape[2] == 1 and w.shape[3] == 1 and groups == 1 and list(stride) == [1, 1]
             and list(padding) == [0, 0])
 
 
