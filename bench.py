@@ -89,31 +89,6 @@ class Workload:
         self.model_dtype, self.describe, self.dist_axis = model_dtype, describe, dist_axis
 
 
-def _clips(n, length=80000, sr=16000, seed=3):
-    """SURVEY 8(d) c3 input: 3 random sinusoids (50-4000 Hz) + 0.1 N(0,1), peak-normalised."""
-    rs = np.random.RandomState(seed)
-    t = np.arange(length) / sr
-    out = np.empty((n, length), dtype=np.float32)
-    for i in range(n):
-        f = rs.uniform(50, 4000, 3)
-        a = rs.uniform(0.2, 1.0, 3)
-        w = (a[:, None] * np.sin(2 * np.pi * f[:, None] * t[None])).sum(0) + 0.1 * rs.standard_normal(length)
-        out[i] = (w / np.abs(w).max()).astype(np.float32)
-    return torch.tensor(out)
-
-
-def _volumes(n, size=128, seed=5):
-    """SURVEY 8(d) c5 input: Gaussian-smoothed N(0,1) thresholded to {0, 1}."""
-    g = torch.Generator().manual_seed(seed)
-    v = torch.randn(n, 1, size, size, size, generator=g)
-    k = torch.tensor([0.25, 0.5, 0.25])
-    for ax in (2, 3, 4):
-        shape = [1, 1, 1, 1, 1]
-        shape[ax] = 3
-        v = torch.nn.functional.conv3d(v, k.view(shape), padding=[1 if a == ax else 0 for a in (2, 3, 4)])
-    return (v > 0).float()
-
-
 def _elephant():
     crop = np.load(os.path.join(REPO, "tests", "golden", "elephant_224.npz"))["crop"].astype(np.float32) / 255.0
     mean = np.array([0.485, 0.456, 0.406], dtype=np.float32)[:, None, None]
@@ -141,7 +116,7 @@ def workload(name):
                         "c2: WAM-2D db4 J=3 SmoothGrad n_samples=25, batch 64 x 224x224, ResNet-50", "images")
     if name == "c3":
         return Workload("c3", 1, "WAM-1D attributions/sec, 5 s 16 kHz clips n_samples=25 (db6 J=5 SmoothGrad, FtEx)",
-                        "attributions/s", 256, 25, lambda: _clips(256),
+                        "attributions/s", 256, 25, lambda: testmodels.audio_clips(256),
                         lambda: [int(v) for v in np.random.RandomState(6).randint(0, 50, 256)],
                         lambda: testmodels.FtEx(seed=0),
                         dict(wavelet="db6", J=5, method="smooth", mode="reflect", n_samples=25, sample_rate=16000,
@@ -161,7 +136,7 @@ def workload(name):
                         "images")
     if name == "c5":
         return Workload("c5", 3, "WAM-3D attributions/sec @128^3 n_samples=25 (haar J=2 SmoothGrad, Voxel3D)",
-                        "attributions/s", 16, 25, lambda: _volumes(16),
+                        "attributions/s", 16, 25, lambda: testmodels.voxel_volumes(16),
                         lambda: [int(v) for v in np.random.RandomState(8).randint(0, 10, 16)],
                         lambda: testmodels.Voxel3D(seed=0),
                         dict(wavelet="haar", J=2, method="smooth", mode="symmetric", n_samples=25,
@@ -187,7 +162,33 @@ def parse(argv=None):
     ap.add_argument("--extras", default="auto", choices=["auto", "off"], help="c2 parity / variants / ceilings")
     ap.add_argument("--dist-axis", default=None, choices=["auto", "samples", "images"])
     ap.add_argument("--wam-probe", action="store_true", help=argparse.SUPPRESS)  # PMC child run
+    # test-only: the process group's backend and every rank on cuda:0 (rehearsing the N > 1 path on
+    # a one-GPU box); the driver's runs use the defaults (RCCL, one GPU per rank)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"], help=argparse.SUPPRESS)
+    ap.add_argument("--single-device", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
+
+
+def self_launch(args, argv):
+    """`bench.py --gpus N` (N > 1) without a torch.distributed launcher: start one process per GPU
+    with torch.distributed.run as a CHILD process -- before this process touches the GPU -- relay
+    rank 0's JSON line and exit with the launcher's status."""
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    log("launching %d ranks: %s" % (args.gpus, " ".join(cmd[1:])))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE)
+    out = p.stdout.decode(errors="replace")
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    if lines:
+        print(lines[-1])
+        sys.stdout.flush()
+    return p.returncode if lines or p.returncode else 1
 
 
 # ============================================================================ explainer
@@ -604,16 +605,25 @@ def main():
     if args.wam_probe:
         return wam_probe(args)
     heartbeat()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return self_launch(args, sys.argv[1:])
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (launch one process per GPU)" % (args.gpus, world))
+    if args.single_device:
+        local = 0
     wl = workload(args.config)
     traffic = None
     if rank == 0 and world == 1 and args.pmc == "auto":
         traffic = live_pmc(args.config)  # child processes, BEFORE this process touches the GPU
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     import wam_amd  # noqa: F401  (fails loudly without libwam_hip.so)
@@ -635,7 +645,8 @@ def main():
             n_local = hi - lo
         else:
             s_local = hi - lo
-    ex = build_explainer(wl, dev, args, dist_on=shard_on, n_local=n_local)
+    # the sample batch is sized from the largest rank's image count, the same on every rank
+    ex = build_explainer(wl, dev, args, dist_on=shard_on, n_local=-(-wl.n // world) if axis == "images" else wl.n)
     log("%s: %d warm-up + %d timed steps on %d GPU(s)" % (wl.name, args.warmup, args.steps, world))
     dt, records, out = timed(lambda: ex(xd, y), args.steps, args.warmup, world, dev)
     assert out is not None
@@ -662,6 +673,17 @@ def main():
             "cold_call_ms": round((time.perf_counter() - t0) * 1e3, 2), "warm_call_ms": round(dt / args.steps * 1e3, 2),
             "what": "timed calls replay the reference's legacy numpy noise stream from the device (drawn once per "
                     "seed / shape / batch, scaled per call, bit-exact); cold_call_ms = one call after clearing it"}
+    if wl.dim == 2:
+        # .scales (lib/wam_2D.py:413,457): the reprojection kernel runs inside every timed call;
+        # its float64 host copy is made on first access -- its cost, outside the timed region:
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        sc = ex.scales
+        secondary["scales_host_copy"] = {
+            "ms": round((time.perf_counter() - t0) * 1e3, 2), "bytes": int(sc.nbytes),
+            "what": ".scales reprojection (k_reproject) runs in every timed call on the device; this is the one-off "
+                    "device -> host float64 copy on first access of ex.scales, not in the timed region"}
+        del sc
     if world > 1:
         secondary["collectives"] = collectives_timing(wl, dev, world, axis)
         exw = build_explainer(wl, dev, args, dist_on=False)  # each rank its own batch, no collective
@@ -707,4 +729,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -262,6 +262,22 @@ int wam_coeff_masks(const wam_plan* plan, int64_t items, const float* coeffs, co
  * HOST arrays of `channels` (<= 4) values. */
 int wam_quantize_normalize(int64_t images, int channels, int64_t plane, const float* rec, const float* mean,
                            const float* std, float* out, void* stream);
+/* The same quantisation followed by torchvision Resize((out_h, out_w)) on the PIL image (Pillow's
+ * 8-bit BILINEAR resample) and ToTensor + Normalize, for reconstructions that are not 224 x 224:
+ * Eval2DWAM's default transform (src/evaluators.py:593-598) on e.g. 256^2 inputs. Replaces the
+ * reference's per-image PIL path (src/evaluators.py:631-633). rec [images, channels, in_h, in_w]
+ * float32 -> out [images, channels, out_h, out_w] float32. The resample tables are Pillow's
+ * (precompute_coeffs + normalize_coeffs_8bpc, wam_amd/evaluation.py pil_bilinear_coeffs): per
+ * output column xx bounds_h[2 xx] = first source column, bounds_h[2 xx + 1] = count, kk_h[xx *
+ * ksize_h + k] = 22-bit fixed-point weights (device int32); likewise vertically with the bounds
+ * relative to source row y0. bounds_h == NULL: the width is unchanged (no horizontal pass; y0 /
+ * tmp_h ignored, bounds_v absolute); bounds_v == NULL: the height is unchanged. tmp_h = source
+ * rows the vertical pass reads (y0 .. y0 + tmp_h - 1). scratch: images * channels * (in_h * in_w +
+ * tmp_h * out_w) bytes. Bit-identical to PIL.Image.resize((out_w, out_h), BILINEAR). */
+int wam_quantize_resize_normalize(int64_t images, int channels, int in_h, int in_w, const float* rec, int out_h,
+                                  int out_w, int ksize_h, const int32_t* bounds_h, const int32_t* kk_h, int ksize_v,
+                                  const int32_t* bounds_v, const int32_t* kk_v, int y0, int tmp_h, const float* mean,
+                                  const float* std, uint8_t* scratch, float* out, void* stream);
 /* scipy.ndimage.gaussian_filter of items h x w float64 maps, mode 'reflect' (half-sample
  * symmetric): weights[0..radius] = the symmetric 1-D kernel (host), axis 0 then axis 1, scipy's
  * accumulation order; tmp: items * h * w doubles of scratch. */

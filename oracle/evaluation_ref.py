@@ -106,9 +106,12 @@ def reconstruct_images(img, J, masks, wavelet="haar"):
 
 
 def to_input(u8, device=None):
-    """Resize((224, 224)) (no-op at 224) + ToTensor + Normalize(ImageNet) of one uint8 image."""
+    """Resize((224, 224)) + ToTensor + Normalize(ImageNet) of one uint8 HWC image, as torchvision does
+    it to the reference's PIL image (src/evaluators.py:593-598): Resize on a PIL image is Pillow's
+    Image.resize((224, 224), BILINEAR) (the identity at 224 x 224) -- run with the real Pillow."""
     if u8.shape[:2] != (224, 224):
-        raise NotImplementedError("restated transform covers 224x224 images (PIL resize is a no-op there)")
+        from PIL import Image
+        u8 = np.asarray(Image.fromarray(np.ascontiguousarray(u8)).resize((224, 224), Image.BILINEAR))
     t = torch.from_numpy(np.ascontiguousarray(u8)).permute(2, 0, 1).contiguous().to(torch.float32).div(255)
     mean = torch.tensor(IMAGENET_MEAN, dtype=torch.float32)[:, None, None]
     std = torch.tensor(IMAGENET_STD, dtype=torch.float32)[:, None, None]

@@ -61,3 +61,62 @@ class AmplitudeToDB(torch.nn.Module):
     def forward(self, x):
         x_db = self.multiplier * torch.log10(torch.clamp(x, min=self.amin))
         return x_db - self.multiplier * self.db_multiplier
+
+
+# ---------------------------------------------------------------------------- librosa mel inversion
+def slaney_mel_basis(sr, n_fft, n_mels):
+    """librosa.filters.mel(sr=sr, n_fft=n_fft, n_mels=n_mels) with its defaults (htk=False:
+    Slaney scale, linear below 1 kHz at 200/3 Hz per mel, logarithmic above with step
+    ln(6.4)/27; fmin 0, fmax sr/2; norm='slaney'), float64, element by element."""
+    import numpy as np
+
+    def hz2mel(f):
+        return f / (200.0 / 3) if f < 1000.0 else 15.0 + math.log(f / 1000.0) / (math.log(6.4) / 27.0)
+
+    def mel2hz(m):
+        return (200.0 / 3) * m if m < 15.0 else 1000.0 * math.exp((math.log(6.4) / 27.0) * (m - 15.0))
+
+    n_f = 1 + n_fft // 2
+    freqs = [i * (sr / 2.0) / (n_f - 1) for i in range(n_f)]
+    lo, hi = hz2mel(0.0), hz2mel(sr / 2.0)
+    pts = [mel2hz(lo + (hi - lo) * k / (n_mels + 1)) for k in range(n_mels + 2)]
+    w = np.zeros((n_mels, n_f))
+    for i in range(n_mels):
+        for j, f in enumerate(freqs):
+            lower = (f - pts[i]) / (pts[i + 1] - pts[i])
+            upper = (pts[i + 2] - f) / (pts[i + 2] - pts[i + 1])
+            w[i, j] = max(0.0, min(lower, upper)) * 2.0 / (pts[i + 2] - pts[i])
+    return w
+
+
+def mel_to_stft(M, sr, n_fft, power=2.0):
+    """librosa.feature.inverse.mel_to_stft (librosa's published algorithm; librosa is absent
+    offline): A = the float32 mel basis; nnls(A, M): x0 = lstsq(A, M) clipped at 0, then scipy
+    L-BFGS-B on 0.5 / M.size * ||A x - M||^2 with bounds x >= 0 and history m = A.shape[1]
+    (one block: the columns fit librosa's 256 KiB block); x ** (1 / power). M [n_mels, T]."""
+    import numpy as np
+    import scipy.optimize
+    A = slaney_mel_basis(sr, n_fft, M.shape[0]).astype(np.float32)
+    B = np.asarray(M, dtype=np.float32)
+    x0 = np.linalg.lstsq(A, B, rcond=None)[0]
+    np.clip(x0, 0, None, out=x0)
+    shape = x0.shape
+
+    def obj(x):
+        x = x.reshape(shape)
+        diff = A @ x - B
+        return (0.5 / B.size) * np.sum(diff ** 2), ((1.0 / B.size) * (A.T @ diff)).ravel()
+    x, _, _ = scipy.optimize.fmin_l_bfgs_b(obj, x0.ravel(), bounds=[(0, None)] * x0.size, m=A.shape[1])
+    return np.power(x.reshape(shape).astype(np.float32), 1.0 / power), A
+
+
+def nnls_exact(A, B):
+    """Column-wise exact NNLS in float64: bounded-variable least squares (scipy.optimize.lsq_linear
+    method='bvls', an active-set method that terminates at the optimum). scipy 1.15's nnls was
+    seen returning non-optimal points on these underdetermined bases, so it is not used."""
+    import numpy as np
+    import scipy.optimize
+    A = np.asarray(A, dtype=np.float64)
+    B = np.asarray(B, dtype=np.float64)
+    return np.stack([scipy.optimize.lsq_linear(A, B[:, j], bounds=(0, np.inf), method="bvls", tol=1e-14,
+                                               max_iter=20 * A.shape[1]).x for j in range(B.shape[1])], 1)

@@ -213,11 +213,16 @@ def single_pass_1d(model, x, y, wavelet, J, mode, n_fft, sample_rate, n_mels, wa
 
 
 def smooth_1d(model, x, y, wavelet="haar", J=3, mode="reflect", n_samples=25, stdev_spread=0.001,
-              random_seed=42, n_fft=1024, sample_rate=44100, n_mels=128):
+              random_seed=42, n_fft=1024, sample_rate=44100, n_mels=128, noise=None):
+    """noise (test hook): float32 [n_samples, N, W] added instead of the legacy numpy stream."""
     if isinstance(x, list):
         x = torch.tensor(np.array([wf / wf.max() for wf in x]).astype(np.float32))
     mels, grads = [], []
-    for _, noisy in legacy_noise_stream(x, n_samples, stdev_spread, random_seed):
+    if noise is not None:
+        stream = ((s, x + torch.from_numpy(np.ascontiguousarray(noise[s]))) for s in range(n_samples))
+    else:
+        stream = legacy_noise_stream(x, n_samples, stdev_spread, random_seed)
+    for _, noisy in stream:
         m, g = single_pass_1d(model, noisy, y, wavelet, J, mode, n_fft, sample_rate, n_mels)
         mels.append(m)
         grads.append(g)
@@ -290,10 +295,21 @@ def single_pass_3d(model, x, y, wavelet, J, mode, input_size, shape=True):
 
 
 def smooth_3d(model, x, y=None, wavelet="haar", J=3, mode="symmetric", n_samples=25,
-              stdev_spread=0.0001, random_seed=42):
+              stdev_spread=0.0001, random_seed=42, noise=None):
+    """noise (test hook): float32 [n_samples, N, D, H, W] added to channel 0 instead of the legacy
+    numpy stream (lib/wam_3D.py:567-579 noises channel 0 only; other channels stay zero)."""
     S = x.shape[-1]
     avg = np.zeros((x.shape[0], S, S, S), dtype=np.float32)
-    for _, noisy in legacy_noise_stream(x, n_samples, stdev_spread, random_seed, item_slice=0):
+    if noise is not None:
+        def _stream():
+            for s in range(n_samples):
+                noisy = torch.zeros(x.shape)
+                noisy[:, 0] = x[:, 0] + torch.from_numpy(np.ascontiguousarray(noise[s]))
+                yield s, noisy
+        stream = _stream()
+    else:
+        stream = legacy_noise_stream(x, n_samples, stdev_spread, random_seed, item_slice=0)
+    for _, noisy in stream:
         avg += single_pass_3d(model, noisy, y, wavelet, J, mode, S)
         for k in range(avg.shape[0]):
             avg[k, :, :] /= n_samples  # legacy: inside the sample loop (lib/wam_3D.py:585-587)

@@ -233,3 +233,29 @@ class Voxel3D(nn.Module):
 
     def forward(self, x):
         return self.model(x)
+
+
+# ------------------------------------------------------------------------------- config inputs
+def audio_clips(n, length=80000, sr=16000, seed=3):
+    """SURVEY 8(d) c3 input: 3 random sinusoids (50-4000 Hz) + 0.1 N(0,1), peak-normalised."""
+    rs = np.random.RandomState(seed)
+    t = np.arange(length) / sr
+    out = np.empty((n, length), dtype=np.float32)
+    for i in range(n):
+        f = rs.uniform(50, 4000, 3)
+        a = rs.uniform(0.2, 1.0, 3)
+        w = (a[:, None] * np.sin(2 * np.pi * f[:, None] * t[None])).sum(0) + 0.1 * rs.standard_normal(length)
+        out[i] = (w / np.abs(w).max()).astype(np.float32)
+    return torch.tensor(out)
+
+
+def voxel_volumes(n, size=128, seed=5):
+    """SURVEY 8(d) c5 input: Gaussian-smoothed N(0,1) thresholded to {0, 1}."""
+    g = torch.Generator().manual_seed(seed)
+    v = torch.randn(n, 1, size, size, size, generator=g)
+    k = torch.tensor([0.25, 0.5, 0.25])
+    for ax in (2, 3, 4):
+        shape = [1, 1, 1, 1, 1]
+        shape[ax] = 3
+        v = torch.nn.functional.conv3d(v, k.view(shape), padding=[1 if a == ax else 0 for a in (2, 3, 4)])
+    return (v > 0).float()

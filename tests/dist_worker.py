@@ -10,7 +10,8 @@ Every rank computes each case twice -- unsharded (dist=None) and sharded (dist=T
 dist_axis) -- and rank 0 writes {case: max |sharded - unsharded| / max(1, max |unsharded|)} plus
 any exception text to OUT.json. Cases cover SURVEY 8(e): ragged sample / step splits, batch
 (image) sharding with the all-reduce MAX of the batch-global maxima, int-y loss scaling with
-unnormalised maps, 1D with fewer samples than ranks (an empty range), 3D legacy weights, IG.
+unnormalised maps, 1D with fewer samples than ranks (an empty range), 3D legacy weights, IG, and
+uneven image splits whose sample range is cut into several chunks (N=23 images, 25 samples).
 """
 import json
 import os
@@ -32,7 +33,18 @@ def cases():
     x96 = torch.tensor(rs.standard_normal((3, 3, 96, 96)).astype(np.float32))
     x1 = torch.tensor(rs.standard_normal((3, 4000)).astype(np.float32))
     x3 = torch.tensor((rs.standard_normal((2, 1, 16, 16, 16)) > 0).astype(np.float32))
+    x23 = torch.tensor(rs.standard_normal((23, 3, 64, 64)).astype(np.float32))
+    y23 = [int(v) for v in rs.randint(0, 10, 23)]
     m2, m1, m3 = testmodels.TinySmooth2D, testmodels.TinyAudio, testmodels.TinyVoxel
+    # uneven image split (12 / 11) with the default (auto) axis and chunk sizes: the ranks must cut
+    # the 25 samples / steps at the same points (rank-local group sizes paired
+    # band-maximum tensors of different sizes in the all-reduce MAX)
+    yield ("2d_smooth_numpy_auto_uneven_23", "2D", m2, x23, y23,
+           dict(wavelet="haar", J=3, n_samples=25, frame="native"))
+    yield ("2d_smooth_philox_auto_uneven_23", "2D", m2, x23, y23,
+           dict(wavelet="db4", J=2, n_samples=25, noise="philox", frame="native"))
+    yield ("2d_ig_auto_uneven_23", "2D", m2, x23, y23,
+           dict(wavelet="haar", J=2, method="integratedgrad", n_samples=25, frame="native"))
     yield ("2d_smooth_numpy_samples", "2D", m2, x2, [1, 4, 2],
            dict(wavelet="haar", J=3, n_samples=5, dist_axis="samples"))
     yield ("2d_smooth_philox_images", "2D", m2, x2, [1, 4, 2],

@@ -126,3 +126,80 @@ def test_gaussian_and_masked_sums_vs_scipy(W):
     check(lib.wam_masked_sums(16, 224 * 224, ptr(src), 28 * 28, ptr(torch.tensor(sub).cuda()), ptr(cell), ptr(sums),
                               stream_of(src.device)))
     assert np.allclose(sums.cpu().numpy(), g["importances"], rtol=1e-12, atol=0)
+
+
+def test_quantize_constant_image_nan_pinned_to_zero(W):
+    """Insertion step 0 masks every coefficient: the reconstruction is all zero and the reference's
+    normalize_data computes 0 / 0 = NaN, which numpy's uint8 cast maps to 0 on x86. The fused
+    k_quantize_normalize pins NaN -> 0 explicitly: the model input is (0 - mean) / std everywhere;
+    a constant non-zero image behaves the same; a regular image is unaffected."""
+    from wam_amd._lib import c_f32, check, lib, ptr, stream_of
+    from wam_amd.evaluation import IMAGENET_MEAN, IMAGENET_STD
+    C, HW = 3, 224 * 224
+    rec = torch.zeros(3, C, HW, device="cuda")
+    rec[1] = 0.37                                       # constant, non-zero
+    rec[2] = torch.rand(C, HW, device="cuda")           # regular
+    out = torch.empty_like(rec)
+    mean, std = (c_f32 * C)(*IMAGENET_MEAN), (c_f32 * C)(*IMAGENET_STD)
+    check(lib.wam_quantize_normalize(3, C, HW, ptr(rec), mean, std, ptr(out), stream_of(rec.device)))
+    want = ((0.0 - torch.tensor(IMAGENET_MEAN)) / torch.tensor(IMAGENET_STD))[:, None].float()
+    for i in (0, 1):
+        assert torch.equal(out[i].cpu(), want.expand(C, HW)), i
+    from oracle import evaluation_ref as E
+    d = np.moveaxis(rec[2].view(C, 224, 224).cpu().numpy(), 0, 2)
+    u8 = (E.normalize_data(d) * 255).astype(np.uint8)
+    ref = E.to_input(u8)
+    assert torch.equal(out[2].view(C, 224, 224).cpu(), ref)
+
+
+@pytest.mark.parametrize("hw", [(256, 256), (230, 230), (112, 112), (300, 200), (224, 257)])
+def test_default_transform_non224_matches_pillow(W, hw):
+    """Eval2DWAM's default transform on a reconstruction that is not 224 x 224 (the reference's
+    Resize((224, 224)) on a PIL image, src/evaluators.py:593-598): the device quantisation + Pillow
+    BILINEAR resample + ToTensor / Normalize equals the real Pillow pipeline bit for bit."""
+    from oracle import evaluation_ref as E
+    from wam_amd._lib import c_f32
+    from wam_amd.evaluation import IMAGENET_MEAN, IMAGENET_STD
+    H, Wd = hw
+    rs = np.random.RandomState(H + Wd)
+    rec = torch.tensor(rs.standard_normal((3, 3, H, Wd)).astype(np.float32)).cuda()
+    rec[1] = 0.25  # a constant reconstruction (insertion step 0): NaN -> 0 bytes
+    ev = W.Eval2DWAM(testmodels.TinySmooth2D().cuda(), wavelet="haar", J=3)
+    got = ev._resize_default(rec, 3, 3, H, Wd, (c_f32 * 3)(*IMAGENET_MEAN), (c_f32 * 3)(*IMAGENET_STD))
+    assert got.shape == (3, 3, 224, 224)
+    for i in range(3):
+        d = np.moveaxis(rec[i].cpu().numpy(), 0, 2)
+        with np.errstate(invalid="ignore"):
+            u8 = (E.normalize_data(d) * 255).astype(np.uint8)
+        assert torch.equal(got[i].cpu(), E.to_input(u8)), i
+
+
+def test_insertion_non224_default_transform_vs_oracle(W):
+    """haar J=3 at 256 x 256 (coefficient array 256 x 256): insertion end to end through the default
+    transform's resize path vs the oracle Eval2DWAM with the real Pillow resize."""
+    from oracle import evaluation_ref as E
+    rs = np.random.RandomState(43)
+    x = torch.tensor(rs.standard_normal((2, 3, 256, 256)).astype(np.float32))
+    y = [1, 5]
+    ev = W.Eval2DWAM(testmodels.TinySmooth2D().cuda(), wavelet="haar", J=3, n_samples=2, tie_order="numpy",
+                     eval_batch=40)
+    scores = ev.insertion(x, y, n_iter=8)
+    ref_scores, ref_curves = E.evaluate_auc(testmodels.TinySmooth2D(), ev.grad_wams, x, y, "insertion", 3, "haar",
+                                            n_iter=8)
+    assert np.abs(np.array(scores) - np.array(ref_scores)).max() < 1e-4
+    for a, b in zip(ev.insertion_curves, ref_curves):
+        assert np.abs(a - b).max() < 1e-4
+
+
+def test_user_transform_receives_pil_image(W):
+    """A user transform gets the reference's PIL image (Image.fromarray of the uint8 HWC array)."""
+    seen = []
+
+    def tf(im):
+        seen.append((type(im).__name__, im.size, im.mode))
+        return torch.tensor(np.asarray(im, dtype=np.float32)).permute(2, 0, 1) / 255.0
+
+    ev = W.Eval2DWAM(testmodels.TinySmooth2D().cuda(), wavelet="haar", J=3, transform=tf)
+    x = torch.rand(1, 3, 224, 224)
+    out = ev._altered_inputs(ev._images(x)[0], torch.ones(2, 224, 224, device="cuda"))
+    assert out.shape == (2, 3, 224, 224) and seen and seen[0] == ("Image", (224, 224), "RGB")

@@ -67,5 +67,57 @@ def test_melspec_filters_and_spectrogram(W):
     assert np.allclose(v.filter_melspec(mel, g, "modulation"), mel * np.abs(gt), rtol=1e-6, atol=0)
     spec = v.spectrogram_from_waveform(x)
     assert spec.shape == (2, 513, 8000 // 256 + 1)
-    with pytest.raises(NotImplementedError):
-        v.compute_spectrogram(mel)
+
+
+def _nnls_obj(A, x, B):
+    return 0.5 * float(np.sum((A.astype(np.float64) @ x.astype(np.float64) - B) ** 2))
+
+
+@pytest.mark.parametrize("sr,n_fft,n_mels,T", [(16000, 256, 32, 24), (16000, 1024, 128, 40), (44100, 512, 64, 17)])
+def test_compute_spectrogram_nnls(W, sr, n_fft, n_mels, T):
+    """compute_spectrogram (lib/wam_1D.py:478-488: librosa mel_to_stft = NNLS of the Slaney mel basis,
+    then sqrt) on the device vs (a) the exact per-frame active-set NNLS (scipy.optimize.nnls) on the
+    same basis: the re-projected mel spectrogram A x is unique and must agree to 1e-4 of max |B|, the
+    objective to 1e-5; (b) the restated librosa L-BFGS-B inversion (oracle/melspec.py): its objective
+    is never below the device one. Parity unpinned (librosa absent): the basis and both solvers are
+    restatements of librosa's published algorithm."""
+    from oracle import melspec as om
+    rs = np.random.RandomState(n_fft)
+    x = rs.standard_normal((2, (T - 1) * (n_fft // 2))).astype(np.float32)
+    v = W.VisualizerWAM1D(testmodels.TinyAudio().cuda(), x, wavelet="haar", J=2, sample_rate=sr, n_fft=n_fft,
+                          n_mels=n_mels)
+    mel = v.compute_melspec(x)                        # torchaudio HTK power mel [2, n_mels, T]
+    assert mel.shape == (2, n_mels, T)
+    spec = v.compute_spectrogram(mel, chunk_size=7)
+    assert spec.shape == (2, n_fft // 2 + 1, T) and spec.dtype == np.float32 and (spec >= 0).all()
+    A = om.slaney_mel_basis(sr, n_fft, n_mels).astype(np.float32)
+    for i in range(2):
+        B = mel[i].astype(np.float64)
+        xg = spec[i].astype(np.float64) ** 2
+        xe = om.nnls_exact(A, B)
+        err = np.abs(A @ xg - A @ xe).max() / np.abs(B).max()
+        fo, fe = _nnls_obj(A, xg, B), _nnls_obj(A, xe, B)
+        assert err <= 1e-4 and fo <= fe * (1 + 1e-5) + 1e-12 * np.sum(B ** 2), (i, err, fo, fe)
+        ref, _ = om.mel_to_stft(mel[i], sr, n_fft)
+        assert fo <= _nnls_obj(A, ref.astype(np.float64) ** 2, B) * (1 + 1e-6)
+    # process_in_chunks (module function, lib/wam_1D.py:442-448): the same per-frame inversion
+    from wam_amd.wam_1D import process_in_chunks
+    pc = process_in_chunks(mel[1], 5, sr, n_fft)
+    assert pc.shape == spec[1].shape and np.abs(pc - spec[1]).max() <= 1e-5 * max(1.0, np.abs(spec[1]).max())
+
+
+def test_filtered_spectrogram_from_melspec(W):
+    """lib/wam_1D.py:619-643 end to end: the source spectrogram is the inversion of the waveform's mel
+    spectrogram, the filtered one the inversion of filter_melspec's output."""
+    rs = np.random.RandomState(5)
+    x = rs.standard_normal((2, 4096)).astype(np.float32)
+    v = W.VisualizerWAM1D(testmodels.TinyAudio().cuda(), x, wavelet="haar", J=2, sample_rate=16000, n_fft=256,
+                          n_mels=32)
+    mel = v.compute_melspec(x)
+    g = rs.standard_normal((2, mel.shape[2], mel.shape[1])).astype(np.float32)
+    src, filt = v.filtered_spectrogram_from_melspec(g, "ht", EPS=0.3, chunk_size=10)
+    assert src.shape == filt.shape == (2, 129, mel.shape[2])
+    assert np.array_equal(src, v.source_spectrograms)
+    assert np.abs(src - v.compute_spectrogram(mel)).max() <= 1e-6 * np.abs(src).max()
+    want = v.compute_spectrogram(v.filter_melspec(mel, g, "ht", EPS=0.3))
+    assert np.abs(filt - want).max() <= 1e-6 * max(1e-30, np.abs(want).max())

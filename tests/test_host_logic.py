@@ -122,6 +122,29 @@ def test_input_gradient_bf16_scale_not_rounded():
     assert torch.equal(g, want.expand(3, 4).contiguous())
 
 
+@pytest.mark.parametrize("y", [3, [1, 4]])
+def test_input_gradient_accumulates_parameter_grads_like_reference(y):
+    """The reference's loss.backward() leaves the model's parameter gradients accumulated in .grad
+    (lib/wam_2D.py:116) over every call; input_gradient over stacked groups leaves their sum."""
+    import testmodels
+    torch.manual_seed(1)
+    groups, n = 3, 2
+    img = torch.randn(groups * n, 3, 32, 32)
+    ref_m, m = testmodels.TinySmooth2D(), testmodels.TinySmooth2D()
+    for s in range(groups):  # the reference: one call (one backward) per sample
+        x = img[s * n:(s + 1) * n].clone().requires_grad_(True)
+        torch.diag(ref_m(x)[:, y]).mean().backward()
+    engine.input_gradient(m, img[:n], y, 1, n)             # a first call ...
+    engine.input_gradient(m, img[n:], y, groups - 1, n)    # ... then two stacked groups: accumulated
+    for (name, p), q in zip(m.named_parameters(), ref_m.parameters()):
+        assert torch.allclose(p.grad, q.grad, rtol=1e-5, atol=1e-7), name
+    frozen = testmodels.TinySmooth2D()
+    for p in frozen.parameters():
+        p.requires_grad_(False)
+    engine.input_gradient(frozen, img, y, groups, n)
+    assert all(p.grad is None for p in frozen.parameters())
+
+
 def test_legacy_noise_stream_matches_reference_loop():
     x = torch.tensor(np.random.RandomState(3).standard_normal((3, 2, 5, 5)).astype(np.float32))
     sig = [float(0.25 * (x[i].max() - x[i].min())) for i in range(3)]
@@ -160,6 +183,33 @@ def test_legacy_noise_device_replay_bit_exact(shape, items, samples):
     engine.clear_noise_cache()
 
 
+@pytest.mark.parametrize("shape,items,samples", [((2, 5, 5), 3, 5), ((7,), 2, 6)])
+def test_legacy_noise_streamed_above_cap_bit_exact(monkeypatch, shape, items, samples):
+    """A draw above the cache cap is streamed chunk by chunk (nothing cached, host and device
+    memory one chunk) and gives the cached form's bits; a rank's later sample range (earlier
+    samples drawn and discarded) too; finish() leaves the global RNG at the reference's end state."""
+    engine.clear_noise_cache()
+    sig = [0.2 + 0.31 * i for i in range(items)]
+    want = dict(engine.legacy_noise(sig, shape, 42, list(range(samples))))
+    end = np.random.get_state()
+    monkeypatch.setattr(engine, "GAUSS_CACHE_BYTES", 8)  # nothing fits
+    for s_lo in (0, 2):
+        np.random.seed(7)
+        ln = engine.LegacyNoise(np.asarray(sig), shape, 42, samples, "cpu")
+        assert ln.streamed and len(engine._GAUSS_CACHE) == 0
+        got = {}
+        for s0, cnt in engine.chunks(s_lo, samples - 1, 2):
+            part = ln.chunk(s0, cnt).numpy()
+            for k in range(cnt):
+                got[s0 + k] = part[k]
+        for s, v in got.items():
+            assert np.array_equal(v, want[s]), (s_lo, s)
+        with pytest.raises(RuntimeError):
+            ln.chunk(0, 1)  # streamed draws go forward only
+        ln.finish()
+        assert _np_state_equal(np.random.get_state(), end)
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("n", [1, 3, 25, 64])
 def test_shard_ranges_partition(world, n):
@@ -186,6 +236,25 @@ def test_sharded_weights_reproduce_sequential_forms():
             avg = (avg + cube[s]) / np.float32(n)
         w3 = engine.legacy3d_weights(0, n, n)
         assert np.allclose((w3[:, None] * cube).sum(0), avg, rtol=1e-5, atol=1e-30)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_image_axis_chunks_rank_independent(world):
+    """dist_axis='images': every rank cuts the sample / step range at the same points whatever its
+    share of an uneven batch (one all-reduce MAX of the band maxima per chunk must pair equal
+    tensors of the same samples)."""
+    from types import SimpleNamespace
+    from wam_amd.wam_2D import WaveletAttribution2D
+    model = torch.nn.Linear(1, 1).eval()
+    for N in range(world, 41):
+        plans = set()
+        for r in range(world):
+            lo, hi = engine.Shard.range_of(r, world, N)
+            shard = SimpleNamespace(world=world, rank=r)
+            n_ref = WaveletAttribution2D._group_items(shard, "images", N, hi - lo)
+            group = engine.auto_group(model, n_ref, None)
+            plans.add(tuple(engine.chunks(0, 25, group)))
+        assert len(plans) == 1, (N, plans)
 
 
 def test_auto_group():
@@ -236,3 +305,26 @@ def test_mel_tables_csr_matches_filterbank():
         assert np.array_equal(tab[:n_fft], win.numpy())
         tw = tab[n_fft:3 * n_fft].reshape(-1, 2)
         assert np.allclose(tw[:, 0] + 1j * tw[:, 1], np.exp(-2j * np.pi * np.arange(n_fft) / n_fft), atol=1e-7)
+
+
+@pytest.mark.parametrize("hw", [(256, 256), (230, 230), (112, 112), (300, 200), (224, 257), (96, 96), (225, 224)])
+def test_pil_bilinear_tables_reproduce_pillow(hw):
+    """Eval2DWAM's default Resize((224, 224)) on non-224 reconstructions (src/evaluators.py:593-598):
+    the host tables (wam_amd.evaluation.pil_bilinear_coeffs) driven through the two fixed-point
+    passes the HIP kernels run (restated here in numpy) give Pillow's own bytes."""
+    from PIL import Image
+    from wam_amd.evaluation import pil_bilinear_coeffs
+    H, W = hw
+    u8 = np.random.RandomState(H * 7 + W).randint(0, 256, (H, W, 3)).astype(np.uint8)
+    ref = np.asarray(Image.fromarray(u8).resize((224, 224), Image.BILINEAR))
+    src = u8.astype(np.int64)
+    half, bits = 1 << 21, 22
+    if W != 224:
+        _, bh, kh = pil_bilinear_coeffs(W, 224)
+        src = np.stack([np.clip((half + (src[:, b0:b0 + c] * kh[x, :c, None]).sum(1)) >> bits, 0, 255)
+                        for x, (b0, c) in enumerate(bh)], 1)
+    if H != 224:
+        _, bv, kv = pil_bilinear_coeffs(H, 224)
+        src = np.stack([np.clip((half + (src[b0:b0 + c] * kv[y, :c, None, None]).sum(0)) >> bits, 0, 255)
+                        for y, (b0, c) in enumerate(bv)], 0)
+    assert np.array_equal(src.astype(np.uint8), ref)

@@ -129,3 +129,31 @@ def test_level_sizes_match_survey():
     assert dwt.level_sizes(80000, L("db6"), 5) == [40005, 20008, 10009, 5010, 2510]
     assert dwt.level_sizes(512, L("sym8"), 5) == [263, 139, 77, 46, 30]
     assert dwt.level_sizes(128, L("haar"), 2) == [64, 32]
+
+
+def test_slaney_mel_basis_restatements_agree():
+    """Row f2's mel inversion basis (librosa.filters.mel defaults, parity unpinned: librosa absent):
+    the oracle's element-by-element restatement and the host table of wam_amd.melspec agree, every
+    triangle has the Slaney area normalisation (peak 2 / (f[i+2] - f[i])), and the scale is linear
+    below 1 kHz."""
+    from oracle import melspec as om
+    from wam_amd import melspec as wm
+    for sr, n_fft, n_mels in [(16000, 256, 32), (44100, 1024, 128), (22050, 2048, 64)]:
+        a, b = om.slaney_mel_basis(sr, n_fft, n_mels), wm.slaney_mel_basis(sr, n_fft, n_mels)
+        assert a.shape == b.shape == (n_mels, 1 + n_fft // 2)
+        assert np.abs(a - b).max() <= 1e-6 * np.abs(a).max()
+        assert (a >= 0).all() and (a.max(axis=1) > 0).all()
+    assert abs(wm._slaney_hz_to_mel(1000.0) - 15.0) < 1e-12 and abs(wm._slaney_hz_to_mel(500.0) - 7.5) < 1e-12
+    assert abs(wm._slaney_mel_to_hz(wm._slaney_hz_to_mel(6400.0)) - 6400.0) < 1e-9
+
+
+def test_librosa_lbfgs_restatement_is_feasible_and_not_better_than_exact_nnls():
+    from oracle import melspec as om
+    rs = np.random.RandomState(2)
+    fb = om.melscale_fbanks(129, 0.0, 8000.0, 32, 16000).numpy()
+    B = (fb.T @ (rs.standard_normal((129, 12)) ** 2 * 50)).astype(np.float32)
+    S, A = om.mel_to_stft(B, 16000, 256)
+    assert S.shape == (129, 12) and (S >= 0).all()
+    xe = om.nnls_exact(A, B)
+    f = lambda x: 0.5 * np.sum((A.astype(np.float64) @ x - B) ** 2)  # noqa: E731
+    assert f(xe) <= f(S.astype(np.float64) ** 2) * (1 + 1e-9)

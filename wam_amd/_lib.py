@@ -72,6 +72,9 @@ _SIGS = {
     "wam_coeff_masks": (c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "wam_quantize_normalize": (c_int, [c_i64, c_int, c_i64, c_vp, ctypes.POINTER(c_f32), ctypes.POINTER(c_f32),
                                        c_vp, c_vp]),
+    "wam_quantize_resize_normalize": (c_int, [c_i64, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_vp,
+                                              c_int, c_vp, c_vp, c_int, c_int, ctypes.POINTER(c_f32),
+                                              ctypes.POINTER(c_f32), c_vp, c_vp, c_vp]),
     "wam_gaussian_filter2d": (c_int, [c_i64, c_int, c_int, c_dp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "wam_upsample_masks": (c_int, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "wam_masked_sums": (c_int, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),

@@ -96,9 +96,96 @@ __global__ void __launch_bounds__(1024) k_quantize_normalize(int channels, int64
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
     const float v = __fdiv_rn(x[i] - mn, rng);
     const float s = __fmul_rn(v, 255.f);
-    const float q = (float)(unsigned char)(int)s;  // astype(uint8): truncation, values in [0, 255]
+    // astype(uint8): truncation, values in [0, 255]. A constant image (e.g. insertion step 0: all
+    // coefficients masked, a zero reconstruction) gives 0 / 0 = NaN, which numpy's NaN -> uint8 cast
+    // turns into 0 on x86 (cvttss2si's 0x80000000, low byte 0): pinned here explicitly rather than
+    // left to the hardware's float -> int conversion of NaN
+    const float q = (s != s) ? 0.f : (float)(unsigned char)(int)s;
     const int c = (int)(i / plane);
     o[i] = __fdiv_rn(__fdiv_rn(q, 255.f) - cn.mean[c], cn.std[c]);
+  }
+}
+
+// ---- torchvision Resize((224, 224)) on the reference's PIL image of a reconstruction that is not
+// 224 x 224 (src/evaluators.py:593-598): normalize_data -> uint8 -> PIL.Image -> Pillow's BILINEAR
+// resample -> ToTensor + Normalize. Pillow's 8-bit resample (libImaging/Resample.c) is integer
+// arithmetic: per output position a run of fixed-point weights (22 fractional bits, built on the
+// host exactly as precompute_coeffs + normalize_coeffs_8bpc do), a horizontal pass into a uint8
+// image of the source rows the vertical pass needs, then the vertical pass; every pass rounds with
+// + 2^21 and clamps (ss >> 22) to [0, 255]. Bit-identical to Pillow (tests/test_gpu_eval.py).
+constexpr int kPilBits = 22;
+
+__device__ __forceinline__ int pil_clip8(int ss) {
+  const int v = ss >> kPilBits;
+  return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+
+// one workgroup per image: the min-max quantisation of k_quantize_normalize, written as bytes
+__global__ void __launch_bounds__(1024) k_quantize_u8(int channels, int64_t plane, const float* __restrict__ rec,
+                                                      uint8_t* __restrict__ u8) {
+  const int64_t n = (int64_t)channels * plane;
+  const float* x = rec + blockIdx.x * n;
+  uint8_t* o = u8 + blockIdx.x * n;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    mn = fminf(mn, x[i]);
+    mx = fmaxf(mx, x[i]);
+  }
+  block_minmax(mn, mx);
+  const float rng = mx - mn;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const float s = __fmul_rn(__fdiv_rn(x[i] - mn, rng), 255.f);
+    o[i] = (s != s) ? (uint8_t)0 : (uint8_t)(int)s;  // NaN (constant image) -> 0, as numpy on x86
+  }
+}
+
+// horizontal pass: planes of in_h x in_w bytes -> tmp planes of tmp_h x out_w (source rows
+// y0 .. y0 + tmp_h - 1)
+__global__ void __launch_bounds__(256) k_pil_resize_h(int64_t planes, int in_h, int in_w, int y0, int tmp_h, int out_w,
+                                                      int ksize, const int32_t* __restrict__ bounds,
+                                                      const int32_t* __restrict__ kk, const uint8_t* __restrict__ src,
+                                                      uint8_t* __restrict__ tmp) {
+  const int64_t total = planes * tmp_h * out_w;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int xx = (int)(t % out_w);
+    const int64_t r = t / out_w;
+    const int y = (int)(r % tmp_h);
+    const int64_t pl = r / tmp_h;
+    const uint8_t* row = src + (pl * in_h + y0 + y) * (int64_t)in_w;
+    const int xmin = bounds[2 * xx], cnt = bounds[2 * xx + 1];
+    const int32_t* k = kk + (int64_t)xx * ksize;
+    int ss = 1 << (kPilBits - 1);
+    for (int x = 0; x < cnt; ++x) ss += (int)row[xmin + x] * k[x];
+    tmp[t] = (uint8_t)pil_clip8(ss);
+  }
+}
+
+// vertical pass (or a copy when the height is unchanged) + ToTensor + Normalize: tmp planes of
+// tmp_h x out_w -> out [images, channels, out_h, out_w] float32
+__global__ void __launch_bounds__(256) k_pil_resize_v_norm(int64_t images, int channels, int tmp_h, int out_h, int out_w,
+                                                           int vertical, int ksize, const int32_t* __restrict__ bounds,
+                                                           const int32_t* __restrict__ kk,
+                                                           const uint8_t* __restrict__ tmp, ChanNorm cn,
+                                                           float* __restrict__ out) {
+  const int64_t total = images * channels * (int64_t)out_h * out_w;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(t % out_w);
+    const int64_t r = t / out_w;
+    const int yy = (int)(r % out_h);
+    const int64_t pl = r / out_h;
+    const int c = (int)(pl % channels);
+    const uint8_t* col = tmp + pl * (int64_t)tmp_h * out_w + x;
+    int u;
+    if (vertical) {
+      const int ymin = bounds[2 * yy], cnt = bounds[2 * yy + 1];
+      const int32_t* k = kk + (int64_t)yy * ksize;
+      int ss = 1 << (kPilBits - 1);
+      for (int y = 0; y < cnt; ++y) ss += (int)col[(int64_t)(ymin + y) * out_w] * k[y];
+      u = pil_clip8(ss);
+    } else {
+      u = col[(int64_t)yy * out_w];
+    }
+    out[t] = __fdiv_rn(__fdiv_rn((float)u, 255.f) - cn.mean[c], cn.std[c]);
   }
 }
 
@@ -204,6 +291,54 @@ int wam_quantize_normalize(int64_t images, int channels, int64_t plane, const fl
   WamTimer tm((hipStream_t)stream, "k_quantize_normalize", 8.0 * images * channels * plane);
   hipLaunchKernelGGL(k_quantize_normalize, dim3((unsigned)images), dim3(1024), 0, (hipStream_t)stream, channels, plane,
                      rec, cn, out);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int wam_quantize_resize_normalize(int64_t images, int channels, int in_h, int in_w, const float* rec, int out_h,
+                                  int out_w, int ksize_h, const int32_t* bounds_h, const int32_t* kk_h, int ksize_v,
+                                  const int32_t* bounds_v, const int32_t* kk_v, int y0, int tmp_h, const float* mean,
+                                  const float* std, uint8_t* scratch, float* out, void* stream) {
+  if (images < 0 || channels < 1 || channels > 4 || in_h < 1 || in_w < 1 || out_h < 1 || out_w < 1 || !rec ||
+      !mean || !std || !scratch || !out)
+    return WAM_ERR_INVALID_ARG;
+  const bool horiz = bounds_h != nullptr, vert = bounds_v != nullptr;
+  if ((horiz && (!kk_h || ksize_h < 1)) || (vert && (!kk_v || ksize_v < 1))) return WAM_ERR_INVALID_ARG;
+  if (!horiz && out_w != in_w) return WAM_ERR_SHAPE;
+  if (!vert && out_h != in_h) return WAM_ERR_SHAPE;
+  if (horiz && (y0 < 0 || tmp_h < 1 || y0 + tmp_h > in_h)) return WAM_ERR_SHAPE;
+  if (images == 0) return WAM_OK;
+  ChanNorm cn{};
+  for (int c = 0; c < channels; ++c) {
+    cn.mean[c] = mean[c];
+    cn.std[c] = std[c];
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t planes = images * channels;
+  const int64_t in_px = planes * (int64_t)in_h * in_w;
+  uint8_t* u8 = scratch;                 // planes x in_h x in_w
+  uint8_t* tmp = scratch + in_px;        // planes x tmp_h x out_w (horizontal pass)
+  {
+    WamTimer tm(st, "k_quantize_u8", 5.0 * in_px);
+    hipLaunchKernelGGL(k_quantize_u8, dim3((unsigned)images), dim3(1024), 0, st, channels, (int64_t)in_h * in_w, rec,
+                       u8);
+    WAM_LAUNCH_CHECK();
+  }
+  const uint8_t* vsrc = u8;
+  int vh = in_h;
+  if (horiz) {
+    const int64_t work = planes * (int64_t)tmp_h * out_w;
+    WamTimer tm(st, "k_pil_resize_h", (double)planes * tmp_h * in_w + (double)work);
+    hipLaunchKernelGGL(k_pil_resize_h, dim3(wam_grid(work, 256)), dim3(256), 0, st, planes, in_h, in_w, y0, tmp_h,
+                       out_w, ksize_h, bounds_h, kk_h, u8, tmp);
+    WAM_LAUNCH_CHECK();
+    vsrc = tmp;
+    vh = tmp_h;
+  }
+  const int64_t work = planes * (int64_t)out_h * out_w;
+  WamTimer tm(st, "k_pil_resize_v_norm", (double)planes * vh * out_w + 4.0 * work);
+  hipLaunchKernelGGL(k_pil_resize_v_norm, dim3(wam_grid(work, 256)), dim3(256), 0, st, images, channels, vh, out_h,
+                     out_w, (int)vert, ksize_v, bounds_v, kk_v, vsrc, cn, out);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }

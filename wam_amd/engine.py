@@ -7,8 +7,13 @@ noise samples (or IG steps) are stacked into ONE model batch of groups x N image
 sum of the per-group losses, so each group gets exactly the gradient of its own reference call
 (models must not couple batch items -- eval-mode BatchNorm is fine; training-mode models are run
 one group per call).
-Only the input gradient is computed (torch.autograd.grad): the reference's parameter-.grad
-accumulation side effect is not reproduced.
+Parameter gradients: the reference's ``loss.backward()`` leaves every parameter that requires
+grad with its gradient accumulated in ``.grad`` (lib/wam_2D.py:116, lib/wam_1D.py:126,
+lib/wam_3D.py:237-238). The same backward here takes ``torch.autograd.grad`` with respect to the
+input and to those parameters and adds the latter into ``.grad`` -- the sum over the stacked
+groups is the sum of the reference's per-call gradients. A model whose parameters are frozen
+(requires_grad False, as the bench does) pays for the input gradient only. ``optimize_model=True``
+runs a folded copy of the model and does not touch the user's parameters.
 """
 import collections
 import contextlib
@@ -67,23 +72,39 @@ def seed_gradient(out, y, groups, n, unit=False, batch=None):
     return go.to(out.dtype), None
 
 
+def trainable_params(model):
+    return [p for p in model.parameters() if p.requires_grad] if isinstance(model, torch.nn.Module) else []
+
+
 def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=False, y_none_mean=False,
-                   input_dtype=None, batch=None):
-    """Gradient of the summed per-group reference losses w.r.t. img (fp32)."""
+                   input_dtype=None, batch=None, params=None):
+    """Gradient of the summed per-group reference losses w.r.t. img (fp32). params (default: the
+    model's parameters that require grad): their gradients are accumulated into .grad, as the
+    reference's loss.backward() does."""
     img = img.detach().requires_grad_(True)
     inp = img if input_dtype is None else img.to(input_dtype)
     inp = inp.contiguous(memory_format=torch.channels_last) if channels_last and img.dim() == 4 else inp
+    params = trainable_params(model) if params is None else list(params)
     ctx = torch.autocast("cuda", dtype=autocast_dtype) if autocast_dtype is not None else contextlib.nullcontext()
-    with ctx:
-        out = model(inp)
-    if y_none_mean:
-        loss = out.float().mean()
-        (g,) = torch.autograd.grad(loss, img)
-    else:
-        seed, scale = seed_gradient(out, y, groups, n, unit=out.dtype != torch.float32, batch=batch)
-        (g,) = torch.autograd.grad(out, img, grad_outputs=seed)
-        if scale is not None:
-            g = g * scale
+    with torch.enable_grad():
+        with ctx:
+            out = model(inp)
+        if y_none_mean:
+            scale = None
+            gs = torch.autograd.grad(out.float().mean(), [img] + params)
+        else:
+            seed, scale = seed_gradient(out, y, groups, n, unit=out.dtype != torch.float32, batch=batch)
+            gs = torch.autograd.grad(out, [img] + params, grad_outputs=seed)
+    g = gs[0]
+    if scale is not None:
+        g = g * scale
+    with torch.no_grad():
+        for p, gp in zip(params, gs[1:]):
+            gp = gp if scale is None else gp * scale
+            if p.grad is None:
+                p.grad = gp.to(p.dtype).clone()
+            else:
+                p.grad.add_(gp.to(p.grad.dtype))
     return g.contiguous()
 
 
@@ -113,9 +134,9 @@ class GradModel:
 
     def __call__(self, img, y, groups, n, y_none_mean=False, batch=None):
         run = self._runner()
-        if self.optimize:
+        if self.optimize:  # a folded copy: the user's parameters are not touched
             return input_gradient(run, img, y, groups, n, None, self.channels_last, y_none_mean,
-                                  input_dtype=self.autocast_dtype, batch=batch)
+                                  input_dtype=self.autocast_dtype, batch=batch, params=[])
         return input_gradient(run, img, y, groups, n, self.autocast_dtype, self.channels_last, y_none_mean,
                               batch=batch)
 
@@ -148,46 +169,91 @@ def clear_noise_cache():
 
 
 class LegacyNoise:
-    """The reference's noise stream (lib/wam_2D.py:385-403, lib/wam_1D.py, lib/wam_3D.py):
-    np.random.seed(seed), then for every sample s and item i in order
+    """The reference's noise stream (lib/wam_2D.py:385-403, lib/wam_1D.py:305-322,
+    lib/wam_3D.py:567-579): np.random.seed(seed), then for every sample s and item i in order
     np.random.normal(0, sigma_i, item_shape) in float64, cast to float32 -- replayed on the device.
 
     numpy's legacy normal is ``loc + scale * gauss`` over the unscaled MT19937 / polar sequence, and
     that sequence depends only on (seed, item size, items, samples), not on the images. It is drawn
-    once with np.random.standard_normal (the same generator calls in the same order), kept on the
-    device in float64 (bounded LRU cache, GAUSS_CACHE_BYTES), and each call scales it there:
-    float32(sigma_i * g) is the reference's value bit for bit (IEEE fp64 product, round-to-nearest
-    cast; 0.0 + v = v). The global numpy RNG is left where the reference leaves it: after all
-    n_samples samples (a cache hit restores that state with np.random.set_state)."""
+    with np.random.standard_normal (the same generator calls in the same order) and scaled on the
+    device: float32(sigma_i * g) is the reference's value bit for bit (IEEE fp64 product,
+    round-to-nearest cast; 0.0 + v = v).
+
+    Two forms, same values:
+    * cached (the whole draw fits GAUSS_CACHE_BYTES): drawn once per (seed, item size, items,
+      samples), kept on the device in float64 (bounded LRU cache);
+    * streamed (larger draws): nothing is kept; chunk() draws the requested samples on the host in
+      stream order (samples before a rank's range are drawn and discarded), uploads and scales
+      them, and drops them -- host and device memory stay at one chunk.
+    The global numpy RNG is left where the reference leaves it, after all n_samples samples: a cache
+    hit restores that state; the streamed form draws the rest of the stream in finish()."""
 
     def __init__(self, sigmas, item_shape, seed, n_samples, device):
         numel = int(np.prod(item_shape))
         items = len(sigmas)
+        self.numel, self.items, self.n_samples = numel, items, int(n_samples)
+        self.device = device
+        self.sigma = torch.tensor([float(v) for v in sigmas], dtype=torch.float64, device=device)
+        self.shape = tuple(item_shape)
+        self.g = None
+        self._rs = None
         key = (int(seed), numel, items, int(n_samples), str(device))
         ent = _GAUSS_CACHE.get(key)
-        if ent is None:
-            np.random.seed(seed)
+        if ent is None and n_samples * items * numel * 8 <= GAUSS_CACHE_BYTES:
+            rs = np.random.RandomState(seed)
             g = np.empty((n_samples, items, numel), dtype=np.float64)
             for s in range(n_samples):
                 for i in range(items):
-                    g[s, i] = np.random.standard_normal(numel)
-            ent = (torch.from_numpy(g).to(device), np.random.get_state())
-            if g.nbytes <= GAUSS_CACHE_BYTES:
-                _GAUSS_CACHE[key] = ent
-                while sum(v[0].numel() * 8 for v in _GAUSS_CACHE.values()) > GAUSS_CACHE_BYTES:
-                    _GAUSS_CACHE.popitem(last=False)
-        else:
+                    g[s, i] = rs.standard_normal(numel)
+            ent = (torch.from_numpy(g).to(device), rs.get_state())
+            _GAUSS_CACHE[key] = ent
+            while sum(v[0].numel() * 8 for v in _GAUSS_CACHE.values()) > GAUSS_CACHE_BYTES:
+                _GAUSS_CACHE.popitem(last=False)
+        if ent is not None:
             _GAUSS_CACHE.move_to_end(key)
             np.random.set_state(ent[1])
-        self.g = ent[0]
-        self.sigma = torch.tensor([float(v) for v in sigmas], dtype=torch.float64, device=self.g.device)
-        self.shape = tuple(item_shape)
+            self.g = ent[0]
+        else:
+            self._rs = np.random.RandomState(seed)   # streamed: private generator, global state at finish()
+            self._next = 0                           # next sample of the stream
+
+    @property
+    def streamed(self):
+        return self.g is None
+
+    def _draw(self, s0, cnt):
+        """float64 standard normals [cnt, items, numel] of samples s0.. (streamed form)."""
+        if s0 < self._next:
+            raise RuntimeError("streamed legacy noise is drawn in sample order (sample %d after %d)"
+                               % (s0, self._next))
+        while self._next < s0:  # samples before the requested range: drawn and discarded
+            for _ in range(self.items):
+                self._rs.standard_normal(self.numel)
+            self._next += 1
+        g = np.empty((cnt, self.items, self.numel), dtype=np.float64)
+        for s in range(cnt):
+            for i in range(self.items):
+                g[s, i] = self._rs.standard_normal(self.numel)
+        self._next += cnt
+        return g
 
     def chunk(self, s0, cnt, i_lo=0, i_hi=None):
         """float32 noise [cnt, items, *item_shape] of samples s0 .. s0+cnt-1, items [i_lo, i_hi)."""
-        i_hi = self.g.shape[1] if i_hi is None else i_hi
-        z = self.g[s0:s0 + cnt, i_lo:i_hi] * self.sigma[i_lo:i_hi, None]
+        i_hi = self.items if i_hi is None else i_hi
+        if self.g is not None:
+            g = self.g[s0:s0 + cnt, i_lo:i_hi]
+        else:
+            g = torch.from_numpy(self._draw(s0, cnt)[:, i_lo:i_hi]).to(self.device)
+        z = g * self.sigma[i_lo:i_hi, None]
         return z.float().view((cnt, i_hi - i_lo) + self.shape)
+
+    def finish(self):
+        """Leave the global numpy RNG at the reference's end state (after all n_samples)."""
+        if self._rs is not None:
+            if self._next < self.n_samples:
+                self._draw(self.n_samples, 0)
+            np.random.set_state(self._rs.get_state())
+            self._rs = None
 
 
 # ------------------------------------------------------------------------------ distribution

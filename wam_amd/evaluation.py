@@ -33,6 +33,7 @@ Normalize(ImageNet)) runs fused on the GPU; a user ``transform`` (a callable on 
 images) is applied on the host instead.
 """
 import ctypes
+import math
 import random
 
 import numpy as np
@@ -100,6 +101,34 @@ def generate_subsets(grid_size, subset_size, sample_size):
             for _ in range(sample_size)]
 
 
+def pil_bilinear_coeffs(in_size, out_size):
+    """Pillow's resample tables for BILINEAR along one axis (libImaging/Resample.c precompute_coeffs
+    with box (0, in_size), then normalize_coeffs_8bpc): (ksize, bounds [out, 2] = (first source
+    index, count), 22-bit fixed-point weights [out, ksize] int64, C truncation of w * 2^22 +- 0.5)."""
+    scale = in_size / out_size
+    filterscale = max(scale, 1.0)
+    support = 1.0 * filterscale                      # the triangle filter's support is 1
+    ksize = int(math.ceil(support)) * 2 + 1
+    kk = np.zeros((out_size, ksize))
+    bounds = np.zeros((out_size, 2), dtype=np.int64)
+    ss = 1.0 / filterscale
+    for xx in range(out_size):
+        center = (xx + 0.5) * scale
+        xmin = max(int(center - support + 0.5), 0)
+        xmax = min(int(center + support + 0.5), in_size) - xmin
+        ww = 0.0
+        for x in range(xmax):
+            t = abs((x + xmin - center + 0.5) * ss)
+            w = 1.0 - t if t < 1.0 else 0.0
+            kk[xx, x] = w
+            ww += w
+        if ww != 0.0:
+            kk[xx, :xmax] /= ww
+        bounds[xx] = (xmin, xmax)
+    fixed = np.trunc(np.where(kk < 0, -0.5 + kk * (1 << 22), 0.5 + kk * (1 << 22))).astype(np.int64)
+    return ksize, bounds, fixed
+
+
 class Eval2DWAM(WaveletAttribution2D):
     """src/evaluators.py:553-801 -- insertion / deletion (Petsiuk et al.), mu-fidelity (Bhatt et al.)."""
 
@@ -162,22 +191,54 @@ class Eval2DWAM(WaveletAttribution2D):
         rh, rw = plan.rec_shape
         if self.transform is not None:
             return self._host_transform(rec.view(M, C, rh, rw))
-        if (rh, rw) != (224, 224):
-            raise NotImplementedError("the fused default transform covers 224x224 reconstructions (Resize((224, "
-                                      "224)) is a no-op there); pass transform= for other sizes")
-        out = torch.empty((M, C, rh, rw), dtype=torch.float32, device=dev)
         mean = (c_f32 * C)(*IMAGENET_MEAN[:C])
         std = (c_f32 * C)(*IMAGENET_STD[:C])
-        check(lib.wam_quantize_normalize(M, C, rh * rw, ptr(rec), mean, std, ptr(out), stream_of(dev)))
+        if (rh, rw) == (224, 224):  # Resize((224, 224)) is the identity: one fused pass
+            out = torch.empty((M, C, rh, rw), dtype=torch.float32, device=dev)
+            check(lib.wam_quantize_normalize(M, C, rh * rw, ptr(rec), mean, std, ptr(out), stream_of(dev)))
+            return out
+        return self._resize_default(rec, M, C, rh, rw, mean, std)
+
+    def _resize_default(self, rec, M, C, rh, rw, mean, std, size=(224, 224)):
+        """The default transform on a reconstruction of another size: uint8 quantisation, Pillow's
+        BILINEAR resample to 224 x 224 (what torchvision's Resize does to the reference's PIL image)
+        and ToTensor + Normalize, on the device (wam_quantize_resize_normalize)."""
+        dev = self._dev
+        oh, ow = size
+        th = tv = None
+        if ow != rw:
+            th = pil_bilinear_coeffs(rw, ow)
+        if oh != rh:
+            tv = pil_bilinear_coeffs(rh, oh)
+        y0, tmp_h = 0, rh
+        if th is not None and tv is not None:  # the horizontal pass covers the rows the vertical one reads
+            b = tv[1]
+            y0, tmp_h = int(b[0, 0]), int(b[-1, 0] + b[-1, 1] - b[0, 0])
+            tv = (tv[0], b - np.array([y0, 0], dtype=b.dtype), tv[2])
+        dv = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.int32)).to(dev)  # noqa: E731
+        bh = kh = bv = kv = None
+        if th is not None:
+            bh, kh = dv(th[1]), dv(th[2])
+        if tv is not None:
+            bv, kv = dv(tv[1]), dv(tv[2])
+        scratch = torch.empty(M * C * (rh * rw + (tmp_h * ow if th is not None else 0)) + 16, dtype=torch.uint8,
+                              device=dev)
+        out = torch.empty((M, C, oh, ow), dtype=torch.float32, device=dev)
+        p_ = lambda t: None if t is None else ptr(t)  # noqa: E731
+        check(lib.wam_quantize_resize_normalize(M, C, rh, rw, ptr(rec), oh, ow, th[0] if th else 0, p_(bh), p_(kh),
+                                                tv[0] if tv else 0, p_(bv), p_(kv), y0, tmp_h, mean, std,
+                                                ptr(scratch), ptr(out), stream_of(dev)))
         return out
 
     def _host_transform(self, rec):
-        """uint8 HWC images exactly as the reference builds them, then the user's transform."""
+        """The reference's PIL images (uint8 HWC -> PIL.Image.fromarray, src/evaluation_helpers.py
+        reconstruct_images), then the user's transform (src/evaluators.py:631-633)."""
+        from PIL import Image
         out = []
         for r in rec.double().cpu().numpy():
             d = np.moveaxis(r, 0, 2).astype(np.float32)
             u8 = (((d - d.min()) / (d.max() - d.min()).astype(np.float32)) * 255).astype(np.uint8)
-            out.append(torch.as_tensor(self.transform(u8)).float())
+            out.append(torch.as_tensor(np.asarray(self.transform(Image.fromarray(u8)))).float())
         return torch.stack(out).to(self._dev)
 
     def _probs(self, inputs, label):

@@ -143,3 +143,113 @@ def melspec_power(wave, n_fft, sample_rate, n_mels):
     if kernel_supported(n_fft, n_mels):
         return _MelFn.apply(wave, n_fft, sample_rate, n_mels, False).transpose(-1, -2)
     return _torch_melspec(wave, n_fft, sample_rate, n_mels, False).transpose(-1, -2)
+
+
+# ------------------------------------------------------------------------------ mel inversion (f2)
+_MELINV = {}
+
+
+def _slaney_hz_to_mel(f):
+    f = np.asanyarray(f, dtype=np.float64)
+    f_sp, min_log_hz = 200.0 / 3, 1000.0
+    min_log_mel, logstep = min_log_hz / f_sp, np.log(6.4) / 27.0
+    return np.where(f >= min_log_hz, min_log_mel + np.log(np.maximum(f, 1e-300) / min_log_hz) / logstep, f / f_sp)
+
+
+def _slaney_mel_to_hz(m):
+    m = np.asanyarray(m, dtype=np.float64)
+    f_sp, min_log_hz = 200.0 / 3, 1000.0
+    min_log_mel, logstep = min_log_hz / f_sp, np.log(6.4) / 27.0
+    return np.where(m >= min_log_mel, min_log_hz * np.exp(logstep * (m - min_log_mel)), f_sp * m)
+
+
+def slaney_mel_basis(sample_rate, n_fft, n_mels):
+    """librosa.filters.mel(sr, n_fft, n_mels) defaults (the basis librosa.feature.inverse.mel_to_stft
+    inverts, lib/wam_1D.py:446): Slaney mel scale (htk=False), fmin 0, fmax sr / 2, triangles over
+    the rfft bin frequencies, 'slaney' area normalisation 2 / (f[i+2] - f[i]); float32 [n_mels,
+    1 + n_fft // 2]. Published algorithm of librosa (absent offline: parity unpinned)."""
+    fftfreqs = np.linspace(0.0, sample_rate / 2.0, 1 + n_fft // 2)
+    mel_f = _slaney_mel_to_hz(np.linspace(_slaney_hz_to_mel(0.0), _slaney_hz_to_mel(sample_rate / 2.0), n_mels + 2))
+    fdiff = np.diff(mel_f)
+    ramps = np.subtract.outer(mel_f, fftfreqs)
+    w = np.zeros((n_mels, 1 + n_fft // 2))
+    for i in range(n_mels):
+        lower = -ramps[i] / fdiff[i]
+        upper = ramps[i + 2] / fdiff[i + 1]
+        w[i] = np.maximum(0, np.minimum(lower, upper))
+    w *= (2.0 / (mel_f[2:n_mels + 2] - mel_f[:n_mels]))[:, None]
+    return w.astype(np.float32)
+
+
+class MelInverse:
+    """Device data of the NNLS mel inversion for one (sr, n_fft, n_mels): the basis A [M, F], its
+    Gram matrix A^T A [F, F], A^T, the minimum-norm least-squares operator pinv(A) [F, M] (librosa's
+    initial point) and the Lipschitz constant ||A||_2^2 of the gradient (float64 SVD on the host)."""
+
+    def __init__(self, sample_rate, n_fft, n_mels, device):
+        A = slaney_mel_basis(sample_rate, n_fft, n_mels)
+        A64 = A.astype(np.float64)
+        self.lip = float(np.linalg.norm(A64, 2) ** 2)
+        self.A = torch.tensor(A, device=device)
+        self.At = self.A.t().contiguous()
+        self.G = torch.tensor((A64.T @ A64).astype(np.float32), device=device)
+        self.pinv = torch.tensor(np.linalg.pinv(A64).astype(np.float32), device=device)
+
+    @staticmethod
+    def get(sample_rate, n_fft, n_mels, device):
+        key = (sample_rate, n_fft, n_mels, torch.device(device))
+        if key not in _MELINV:
+            _MELINV[key] = MelInverse(sample_rate, n_fft, n_mels, device)
+        return _MELINV[key]
+
+
+def nnls_mel(inv, B, max_iter=3000, tol=1e-6):
+    """min_x 0.5 ||A x - B||^2 s.t. x >= 0, column by column, B [..., M, T] (device) -> x [..., F, T].
+
+    librosa's nnls (the algorithm lib/wam_1D.py:446 runs) starts from the clipped minimum-norm
+    least-squares solution and runs scipy's L-BFGS-B. Here every column of the batch runs FISTA
+    (accelerated projected gradient, step 1 / ||A||^2, gradient-restarted momentum) from the same
+    initial point; each iteration is one GEMM with the Gram matrix (hipBLASLt) plus elementwise
+    updates. The mel basis has more bins than bands, so the minimiser x is not unique, but its
+    re-projection A x is (the objective is strictly convex in A x): that is what the tests compare.
+    Stops when the KKT residual max |min(x, grad)| of every column is <= tol * max |A^T B| or
+    after max_iter iterations. librosa's L-BFGS-B stops at an absolute projected-gradient tolerance
+    (pgtol 1e-5 on an objective scaled by 1 / B.size), i.e. earlier and data-scale dependent: its
+    objective is never below the NNLS optimum this converges to (tests/test_gpu_visual1d.py)."""
+    shape = B.shape
+    M, T = shape[-2], shape[-1]
+    Bc = B.reshape(-1, M, T).permute(1, 0, 2).reshape(M, -1).to(torch.float32)   # [M, cols]
+    AtB = inv.At @ Bc                                                              # [F, cols]
+    x = torch.clamp(inv.pinv @ Bc, min=0.0)
+    y = x.clone()
+    t = torch.ones(x.shape[1], dtype=torch.float32, device=x.device)   # momentum per column
+    step = 1.0 / inv.lip
+    scale = float(AtB.abs().max()) if AtB.numel() else 0.0  # the gradient's scale at x = 0
+    stop = tol * max(scale, 1e-30)
+    for it in range(max_iter):
+        grad = inv.G @ y - AtB
+        x_new = torch.clamp(y - step * grad, min=0.0)
+        if it % 25 == 24:  # the only host synchronisation: the KKT residual every 25 iterations
+            kkt = torch.minimum(x_new, inv.G @ x_new - AtB).abs().max()
+            if float(kkt) <= stop:
+                x = x_new
+                break
+        # gradient restart per column (O'Donoghue & Candes): momentum dropped where it points uphill
+        d = x_new - x
+        restart = (grad * d).sum(0) > 0
+        t_new = 0.5 * (1.0 + torch.sqrt(1.0 + 4.0 * t * t))
+        beta = torch.where(restart, torch.zeros_like(t), (t - 1.0) / t_new)
+        t = torch.where(restart, torch.ones_like(t), t_new)
+        y = x_new + beta * d
+        x = x_new
+    F = x.shape[0]
+    return x.reshape(F, -1, T).permute(1, 0, 2).reshape(shape[:-2] + (F, T))
+
+
+def mel_to_stft(M, sample_rate, n_fft, power=2.0):
+    """librosa.feature.inverse.mel_to_stft(M, sr, n_fft) (power 2): NNLS of the Slaney mel basis,
+    then x ** (1 / power). M [..., n_mels, T] on the device."""
+    require_cuda(M, "mel spectrogram")
+    inv = MelInverse.get(sample_rate, n_fft, M.shape[-2], M.device)
+    x = nnls_mel(inv, M)
+    return x.pow(1.0 / power)

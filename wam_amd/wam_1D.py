@@ -17,6 +17,25 @@ from .melspec import kernel_supported, mel_adjoint, mel_forward, melspec_db
 from .plan import CAP_NOISY_WAVEDEC, accumulate_f32, get_plan, item_sigma, noise_add, trapz_stream
 
 
+def normalize(data):
+    """lib/wam_1D.py:439-440 (min-max over the whole array)."""
+    return (data - np.min(data)) / (np.max(data) - np.min(data))
+
+
+def process_in_chunks(melspec, chunk_size, sr, n_fft):
+    """lib/wam_1D.py:442-448: librosa.feature.inverse.mel_to_stft of a [n_mels, T] power mel
+    spectrogram in time chunks of chunk_size frames -> [1 + n_fft // 2, T] magnitudes. The device
+    NNLS (wam_amd.melspec.mel_to_stft) solves every frame independently, so the chunks are one
+    batch here; chunk_size only keeps the reference's signature."""
+    from .melspec import mel_to_stft
+    if int(chunk_size) < 1:
+        raise ValueError("range() arg 3 must not be zero")
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
+    m = torch.as_tensor(np.asarray(melspec, dtype=np.float32))
+    m = m.to(require_gpu_device(dev or "cpu"))
+    return mel_to_stft(m, sr, n_fft).cpu().numpy()
+
+
 def _peak_normalise(x):
     return torch.tensor(np.array([wf / wf.max() for wf in x]).astype(np.float32))
 
@@ -207,6 +226,8 @@ class WaveletAttribution1D(BaseWAM1D):
                 src = cg[cnt * n * plan.band_offsets[b]:cnt * n * (plan.band_offsets[b] + nb)]
                 accumulate_f32(src, cnt, c_acc[n * plan.band_offsets[b]:n * (plan.band_offsets[b] + nb)])
             self.wam._record(plan, flat, cnt * n, (cnt - 1) * n, cg, cnt * n, (cnt - 1) * n, n)
+        if legacy is not None:
+            legacy.finish()
         shard.all_reduce_sum(mel_acc)
         shard.all_reduce_sum(c_acc)
         accumulate_f32(mel_acc, 0, mel_acc, scale=float(self.n_samples))
@@ -274,8 +295,9 @@ class VisualizerWAM1D(WaveletAttribution1D):
     spectrogram. The reference's spectrograms come from librosa (absent offline, parity
     unpinned): ``spectrogram_from_waveform`` restates librosa.stft's magnitude (hann window,
     centred, constant padding -- librosa >= 0.10 -- hop n_fft // 4) with torch.stft on the GPU;
-    ``compute_spectrogram`` needs librosa's NNLS mel inversion (mel_to_stft) and raises
-    NotImplementedError, so ``filtered_spectrogram_from_melspec`` does too."""
+    ``compute_spectrogram`` is librosa's mel_to_stft (NNLS of the Slaney mel basis, then sqrt) as a
+    batched device solver (wam_amd.melspec.nnls_mel), which ``filtered_spectrogram_from_melspec``
+    uses on the source and the filtered mel spectrograms."""
 
     def __init__(self, model, x, wavelet="haar", J=3, method="smooth", mode="reflect", device=None,
                  approx_coeffs=False, n_mels=128, n_fft=1024, sample_rate=44100, n_samples=25, stdev_spread=0.001,
@@ -296,8 +318,14 @@ class VisualizerWAM1D(WaveletAttribution1D):
         return melspec_power(self._wave(x), self.n_fft, self.sample_rate, self.n_mels).cpu().numpy()
 
     def compute_spectrogram(self, melspecs, chunk_size=100):
-        raise NotImplementedError("compute_spectrogram inverts mel spectrograms with librosa.feature.inverse."
-                                  "mel_to_stft (NNLS on librosa's own mel basis); librosa is not available")
+        """lib/wam_1D.py:478-488: the STFT magnitudes of power mel spectrograms [N, n_mels, T] by
+        librosa.feature.inverse.mel_to_stft (NNLS on librosa's Slaney mel basis, then sqrt), all
+        waveforms and frames in one device batch -> [N, 1 + n_fft // 2, T] float32."""
+        from .melspec import mel_to_stft
+        if int(chunk_size) < 1:
+            raise ValueError("range() arg 3 must not be zero")
+        m = torch.as_tensor(np.asarray(melspecs, dtype=np.float32)).to(self._dev)
+        return mel_to_stft(m, self.sample_rate, self.n_fft).cpu().numpy()
 
     def filter_melspec(self, audio_melspecs, grad_melspecs, filtering_method, EPS=0.2):
         """lib/wam_1D.py:491-519 (hard threshold of the min-max-normalised gradient, or modulation)."""

@@ -311,11 +311,17 @@ class WaveletAttribution2D(BaseWAM2D):
                              normalize_coeffs=normalize_coeffs, frame=frame, autocast_dtype=autocast_dtype,
                              channels_last=channels_last, _grad=self._grad)
         self._avg_dev = None
+        self._scales_res = None
 
-    # ------------------------------------------------------------------ .scales (lazy)
+    # ------------------------------------------------------------------ .scales
+    # The reference recomputes self.scales = reproject_wam(result) at the end of every SmoothGrad /
+    # IG call (lib/wam_2D.py:413,457). Here the reprojection runs inside the call on the device
+    # (k_reproject); the float64 host copy is made on first access of .scales.
     @property
     def scales(self):
-        if self._scales is None and self._avg_dev is not None:
+        if self._scales is None and self._scales_res is not None:
+            self._scales = self._scales_host(self._scales_res, self.J, self.approx_coeffs)
+        elif self._scales is None and self._avg_dev is not None:
             self._scales = self._reproject_dev(self._avg_dev, self.J, self.approx_coeffs)
         return self._scales
 
@@ -326,6 +332,9 @@ class WaveletAttribution2D(BaseWAM2D):
     def _set_result(self, avg_dev):
         self._avg_dev = avg_dev
         self._scales = None
+        self._scales_res = None
+        if avg_dev.shape[1] == avg_dev.shape[2]:
+            self._scales_res = reproject_scales(avg_dev.contiguous(), self.J, self.approx_coeffs)
 
     # ------------------------------------------------------------------ estimators
     def _wam_group(self, plan, n, c, model_group, total):
@@ -341,6 +350,14 @@ class WaveletAttribution2D(BaseWAM2D):
         for s0, cnt in chunks(0, groups, model_group):
             out[s0 * n:(s0 + cnt) * n] = self._grad(imgs[s0 * n:(s0 + cnt) * n], y, cnt, n, batch=batch)
         return out
+
+    @staticmethod
+    def _group_items(shard, axis, N, n):
+        """Image count that sizes the sample / step chunks. On the images axis it is the largest
+        rank's share ceil(N / world), the same on every rank, so all ranks cut the sample range
+        at the same points and issue the same collectives (a rank-local count would pair
+        band-maximum tensors of different sizes and samples across ranks)."""
+        return -(-N // shard.world) if axis == "images" else n
 
     def _split(self, n, n_steps):
         """(shard, axis, image range, sample/step range) of this rank."""
@@ -370,9 +387,12 @@ class WaveletAttribution2D(BaseWAM2D):
         xs, sigma = x[i_lo:i_hi], sigma_all[i_lo:i_hi]
         batch = (i_lo, N) if axis == "images" else None
         gmap, (rh, rw) = frames.smooth_frame(plan, n, self.frame, dev)
-        group = auto_group(self.model, n, self.sample_batch)
+        # chunk sizes from a rank-independent image count: on the images axis every rank must cut
+        # the sample range at the same points (one all-reduce MAX of the band maxima per chunk)
+        n_ref = self._group_items(shard, axis, N, n)
+        group = auto_group(self.model, n_ref, self.sample_batch)
         # parity mode streams the host-generated legacy noise one model group at a time
-        wgroup = group if self.noise == "numpy" else self._wam_group(plan, n, c, group, s_hi - s_lo)
+        wgroup = group if self.noise == "numpy" else self._wam_group(plan, n_ref, c, group, s_hi - s_lo)
         frame = torch.zeros(n * rh * rw, dtype=torch.float64, device=dev)
         legacy = None
         if self.noise == "numpy":
@@ -396,6 +416,8 @@ class WaveletAttribution2D(BaseWAM2D):
             frame_accumulate(cnt, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, frame)
             last = (plan, flat, None, cnt * n * c, (cnt - 1) * n, n, c)
             last_g = g[(cnt - 1) * n:].reshape((n * c,) + rec)
+        if legacy is not None:
+            legacy.finish()
         if last is not None:
             self.wam._record_pass(*last, grad_img=last_g)
         if axis == "images":
@@ -423,8 +445,9 @@ class WaveletAttribution2D(BaseWAM2D):
         base = torch.zeros(n * rh * rw, dtype=torch.float64, device=dev)
         frame_accumulate(1, n, bmap, zmaps, plan.coeff_numel, zmax, plan.nbands, True, base)
         alphas = np.linspace(0, 1, self.n_samples)
-        group = auto_group(self.model, n, self.sample_batch)
-        wgroup = self._wam_group(plan, n, c, group, k_hi - k_lo)
+        n_ref = self._group_items(shard, axis, N, n)
+        group = auto_group(self.model, n_ref, self.sample_batch)
+        wgroup = self._wam_group(plan, n_ref, c, group, k_hi - k_lo)
         acc = torch.zeros(n * rh * rw, dtype=torch.float32, device=dev)
         prev = torch.zeros_like(acc)
         rec = plan.rec_shape
@@ -472,10 +495,15 @@ class WaveletAttribution2D(BaseWAM2D):
 
     # ------------------------------------------------------------------ reprojection
     def _reproject_dev(self, avg_dev, num_levels, approx_coeffs):
-        n, size = avg_dev.shape[0], avg_dev.shape[1]
-        if avg_dev.shape[2] != size:
+        if avg_dev.shape[2] != avg_dev.shape[1]:
             raise NotImplementedError("reproject_wam on a non-square map")
-        sc = reproject_scales(avg_dev.contiguous(), self.J, approx_coeffs).cpu().numpy()
+        return self._scales_host(reproject_scales(avg_dev.contiguous(), self.J, approx_coeffs), num_levels,
+                                 approx_coeffs)
+
+    def _scales_host(self, sc_dev, num_levels, approx_coeffs):
+        """device reprojection [N, J(+1), S, S] -> the reference's .scales array (levels as asked)."""
+        n, size = sc_dev.shape[0], sc_dev.shape[2]
+        sc = sc_dev.cpu().numpy()
         out = np.zeros((n, num_levels + 1 if approx_coeffs else num_levels, size, size))
         for j in range(self.J):
             if j >= out.shape[1]:

@@ -312,6 +312,8 @@ class WaveletAttribution3D(BaseWAM3D):
                 self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 1, weights=w)
             self.wam._coeffs_src = (plan, flat, cnt * n * c, (cnt - 1) * n, n, c)
             self.wam._coeffs = None
+        if legacy is not None:
+            legacy.finish()
         shard.all_reduce_sum(acc)
         self._cube_dev = acc.view(n, S, S, S)
         out = self._cube_dev.cpu().numpy()
