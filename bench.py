@@ -269,8 +269,62 @@ def unit_bytes(wl, kname, units_per_launch, lib_bytes, n_items):
 
 
 # FFT front-end kernels (wam_amd/csrc/melspec.hip): VALU / LDS bound by construction (two to three
-# 512-point FFTs per 4 KB frame), reported beside the HBM roofline rather than as its kernel
-VALU_BOUND = ("k_mel_fwd", "k_mel_adj")
+# 512-point FFTs per 4 KB frame), reported beside the HBM roofline rather than as its kernel, on
+# their own compute roofline (mel_roofline)
+VALU_BOUND = ("k_mel_fwd", "k_mel_adj", "k_mel_fold")
+FP32_PEAK_TFLOPS = 157.3          # MI355X vector fp32 (MI355X_MICROARCH.md)
+LDS_PEAK_TBS = 128 * 256 * 2.4e9 / 1e12   # 128 B/clk/CU (ds_read_b32 / mixed rate) x 256 CUs x 2.4 GHz
+
+
+def mel_frame_model(n_fft, n_mels, nnz, adjoint):
+    """FLOPs and LDS bytes per frame of the mel kernels (the model the report prices them on):
+    an M = n_fft / 2 point complex FFT = 5 M log2 M flops in ceil(log2 M / 3) radix-8 Stockham
+    stages, each reading and writing M complex values (8 B) plus 7/8 M table twiddles after the first;
+    the real-spectrum unpack 10 flops and 3 LDS reads per bin, |X|^2 3 flops per bin, the band sums
+    2 flops and 12 B per filterbank nonzero; the adjoint adds the second FFT, the by-bin sums, the
+    A = 2 dL/dP X products (4 flops per bin) and the Hermitian pack (10 flops, 2 reads per point)."""
+    M = n_fft // 2
+    lg = int(np.log2(M))
+    stages = -(-lg // 3)
+    fft_flops = 5.0 * M * lg
+    fft_lds = stages * 16.0 * M + (stages - 1) * 7.0 * M
+    bins = M + 1
+    flops = n_fft + fft_flops + 13.0 * bins + 2.0 * nnz + 2.0 * n_mels
+    lds = 8.0 * M + fft_lds + 24.0 * bins + 4.0 * bins + 12.0 * nnz
+    if adjoint:
+        flops += fft_flops + 2.0 * nnz + 4.0 * bins + 10.0 * M + n_fft + 4.0 * n_mels
+        lds += fft_lds + 12.0 * nnz + 8.0 * bins + 16.0 * M + 8.0 * M + 4.0 * n_mels
+    return flops, lds
+
+
+def mel_roofline(wl, kern):
+    """compute roofline of the mel kernels at c3: FLOPs / frame (model above), achieved TFLOP/s vs the
+    fp32 vector peak and LDS bytes / s vs the LDS array rate"""
+    if wl.name != "c3":
+        return None
+    from wam_amd.melspec import MelTables
+    n_fft, n_mels, T = 1024, 128, 80000
+    F = T // (n_fft // 2) + 1
+    nnz = MelTables.get(n_fft, n_mels, 16000, "cpu").nnz
+    out = {}
+    for n in ("k_mel_fwd", "k_mel_adj"):
+        if n not in kern:
+            continue
+        k = kern[n]
+        per_item = 4.0 * T * (2 if n == "k_mel_adj" else 1) + 4.0 * F * n_mels   # the library's bytes per clip
+        frames = k["bytes_per_launch"] / per_item * F
+        fl, lb = mel_frame_model(n_fft, n_mels, nnz, n == "k_mel_adj")
+        sec = k["mean_us"] * 1e-6
+        out[n] = {"frames_per_launch": round(frames), "flops_per_frame": round(fl), "lds_bytes_per_frame": round(lb),
+                  "mean_us": round(k["mean_us"], 2), "achieved_tflops": round(frames * fl / sec / 1e12, 2),
+                  "fp32_peak_tflops": FP32_PEAK_TFLOPS,
+                  "frac_fp32": round(frames * fl / sec / 1e12 / FP32_PEAK_TFLOPS, 4),
+                  "lds_tbs": round(frames * lb / sec / 1e12, 2), "lds_peak_tbs": round(LDS_PEAK_TBS, 1),
+                  "frac_lds": round(frames * lb / sec / 1e12 / LDS_PEAK_TBS, 4)}
+    if "k_mel_fold" in kern:
+        out["k_mel_fold"] = {"mean_us": round(kern["k_mel_fold"]["mean_us"], 2),
+                             "note": "frames 0 and F-1 of every clip recomputed for the reflect folds"}
+    return out or None
 
 
 def traffic_table(kern, traffic):
@@ -305,8 +359,7 @@ def roofline(wl, kern, steps, units_per_step, traffic, n_items):
             "library_bytes_per_launch": round(kd["bytes_per_launch"]), "library_GBps": round(kd["GBps"], 1),
             "mean_us": round(kd["mean_us"], 2),
             "wam_ms_per_step": round(sum(k["total_ms"] for k in kern.values()) / steps, 3),
-            "valu_bound_kernels": {n: {"mean_us": round(kern[n]["mean_us"], 2), "launches": kern[n]["launches"]}
-                                   for n in VALU_BOUND if n in kern} or None,
+            "valu_bound_kernels": mel_roofline(wl, kern),
             "traffic_by_kernel": traffic_table(kern, traffic),
             "kernels": {n: {kk: round(vv, 3) for kk, vv in k.items()} for n, k in
                         sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"])}}

@@ -112,7 +112,7 @@ def test_c3_db6_j5_80k_philox(W):
     x = testmodels.audio_clips(2)
     y = [3, 7]
     S = 2
-    noise = _philox_noise(x, 0.001, S, 80000, (S, 2, 80000))
+    noise = _philox_noise(x, 0.001, S, 80000, (2, 80000))
     ref_mel, ref_c = wam_ref.smooth_1d(testmodels.TinyAudio(), x, y, n_samples=S, noise=noise, **C3_KW)
     ex = W.WaveletAttribution1D(testmodels.TinyAudio().cuda(), n_samples=S, noise="philox", **C3_KW)
     mel, cs = ex(x, y)
@@ -149,7 +149,7 @@ def test_c5_haar_j2_128_philox(W):
     x = testmodels.voxel_volumes(2)
     y = [3, 5]
     S = 3
-    noise = _philox_noise(x, 1e-4, S, 128 ** 3, (S, 2, 128, 128, 128))
+    noise = _philox_noise(x, 1e-4, S, 128 ** 3, (2, 128, 128, 128))
     ref = wam_ref.smooth_3d(testmodels.TinyVoxel(), x, y, n_samples=S, noise=noise, **C5_KW)
     ex = W.WaveletAttribution3D(testmodels.TinyVoxel().cuda(), n_samples=S, noise="philox", sample_batch=2,
                                 **C5_KW)

@@ -100,10 +100,16 @@ def test_compute_spectrogram_nnls(W, sr, n_fft, n_mels, T):
         assert err <= 1e-4 and fo <= fe * (1 + 1e-5) + 1e-12 * np.sum(B ** 2), (i, err, fo, fe)
         ref, _ = om.mel_to_stft(mel[i], sr, n_fft)
         assert fo <= _nnls_obj(A, ref.astype(np.float64) ** 2, B) * (1 + 1e-6)
-    # process_in_chunks (module function, lib/wam_1D.py:442-448): the same per-frame inversion
+    # process_in_chunks (module function, lib/wam_1D.py:442-448): the same per-frame inversion in
+    # chunks of 5 frames. The minimiser is not unique (more bins than bands) and the solver stops on
+    # the worst column of a chunk, so chunkings agree on the re-projection A x (unique), not on x
     from wam_amd.wam_1D import process_in_chunks
     pc = process_in_chunks(mel[1], 5, sr, n_fft)
-    assert pc.shape == spec[1].shape and np.abs(pc - spec[1]).max() <= 1e-5 * max(1.0, np.abs(spec[1]).max())
+    assert pc.shape == spec[1].shape and pc.dtype == np.float32 and (pc >= 0).all()
+    B = mel[1].astype(np.float64)
+    rp = A.astype(np.float64) @ (pc.astype(np.float64) ** 2)
+    rs_ = A.astype(np.float64) @ (spec[1].astype(np.float64) ** 2)
+    assert np.abs(rp - rs_).max() <= 2e-4 * np.abs(B).max(), np.abs(rp - rs_).max() / np.abs(B).max()
 
 
 def test_filtered_spectrogram_from_melspec(W):

@@ -13,8 +13,9 @@
 // recomputes the frame, forms G[k] = 2 dL/dP[k] X[k] and evaluates
 //   g_frame[n] = w[n] Re(sum_{k=0..M} G[k] e^{+2 pi i k n/N})
 // with one inverse M-point FFT of the Hermitian-packed spectrum; the reflect padding is folded
-// back when the frames are overlap-added. Workgroups own runs of hop-blocks of the output and keep
-// the frames touching them in LDS, so every output sample is written once, in a fixed order.
+// back when the frames are overlap-added. A wave owns a run of hop-blocks of the output and streams
+// its frames in order, keeping the previous frame's second half in registers, so every output sample
+// is written once, in a fixed order (k_mel_adj_run); the reflect folds follow (k_mel_fold).
 //
 // tables (device, float): window[N] | twiddle[2N] (cos, sin of -2 pi m / N) | band_w[nnz] | bin_w[nnz]
 // index  (device, int32): band_ptr[n_mels+1] | band_bin[nnz] | bin_ptr[N/2+2] | bin_band[nnz]
@@ -29,12 +30,10 @@
 namespace {
 
 constexpr int kWavesF = 4;  // forward: waves per workgroup, each streaming frames (one frame per wave at a time)
-constexpr int kWavesA = 8;  // adjoint: waves per workgroup sharing the run's frame slots
 
 struct MelGeom {
   int64_t items, T;
   int F, hop, n_mels, nnz;
-  int blocks_per_wg, wg_per_item;  // adjoint
   int to_db;
 };
 
@@ -57,7 +56,7 @@ __device__ __forceinline__ float2 muls(float2 v) {
 }
 
 // LDS index padding: breaks the stride-R writes of the first stages across banks
-__device__ __forceinline__ int pad(int i) { return i + (i >> 4); }
+__host__ __device__ __forceinline__ int pad(int i) { return i + (i >> 4); }
 
 template <int S>
 __device__ __forceinline__ void dft2(float2* a) {
@@ -334,12 +333,13 @@ __global__ void __launch_bounds__(64 * kWavesF) k_mel_fwd(MelGeom g, const float
   }
 }
 
-// one frame's gradient g_frame[N] into slot (the whole adjoint chain of the frame, see header);
-// the frame's samples are in `in`, which is refilled with frame f_next (if >= 0) meanwhile
+// one frame's adjoint chain (see header) up to the inverse FFT, whose output z stays in buf: the
+// frame's gradient is g[2n] = w[2n] z[n].x / 2, g[2n+1] = w[2n+1] z[n].y / 2; the frame's samples are
+// in `in`, which is refilled with frame f_next (if >= 0) meanwhile
 template <int LOGN>
-__device__ void frame_adjoint(const MelGeom& g, const Tabs& t, FrameIn<LOGN>& in, const float* __restrict__ x,
-                              int f, int f_next, const float* __restrict__ gdb, float2* buf, float* gmel, float* slot,
-                              int lane) {
+__device__ __forceinline__ void frame_adjoint_buf(const MelGeom& g, const Tabs& t, FrameIn<LOGN>& in,
+                                                  const float* __restrict__ x, int f, int f_next,
+                                                  const float* __restrict__ gdb, float2* buf, float* gmel, int lane) {
   constexpr int M = 1 << (LOGN - 1), KI = M / 64 + 1;
   constexpr int kMelRegs = 4;  // bands lane + 64 j, j < 4, held in registers (n_mels <= 256)
   in.store(t.win, buf, lane);
@@ -380,6 +380,7 @@ __device__ void frame_adjoint(const MelGeom& g, const Tabs& t, FrameIn<LOGN>& in
       if (k == 0 || k == M) A[i] = make_float2(2.f * A[i].x, 0.f);
     }
   }
+  wave_sync();  // gmel may live in buf's tail (the run kernel): all reads before A overwrites it
 #pragma unroll
   for (int i = 0; i < KI; ++i)
     if (lane + 64 * i <= M) buf[pad(lane + 64 * i)] = A[i];
@@ -402,64 +403,154 @@ __device__ void frame_adjoint(const MelGeom& g, const Tabs& t, FrameIn<LOGN>& in
     if (lane + 64 * i < M) buf[pad(lane + 64 * i)] = Zp[i];
   wave_sync();
   fft_stages<LOGN, 0, 1>(buf, t.tw, lane);
-  float2* s2 = reinterpret_cast<float2*>(slot);
-  for (int n = lane; n < M; n += 64) {
-    const float2 z = buf[pad(n)];
-    s2[n] = make_float2(t.win[2 * n] * (0.5f * z.x), t.win[2 * n + 1] * (0.5f * z.y));
-  }
-  wave_sync();
 }
 
-// grid: wg_per_item x items workgroups; workgroup (c, it) owns hop-blocks [c * BPW, (c + 1) * BPW)
+// ------------------------------------------------------------------------------------------------
+// Run-streaming adjoint (the default). A wave owns a run of consecutive hop-blocks [b0, b1) of one
+// waveform and computes the frames b0 .. min(b1, F - 1) in order; frame f's gradient leaves the
+// inverse FFT as samples 2n, 2n + 1 of lane n mod 64 (n = lane + 64 j), so its second half stays
+// in registers (`carry`) and block f - 1 = carry + the next frame's first half is written straight
+// to HBM with coalesced float2 stores, once, in the slot kernel's summation order. No frame slots
+// and no workgroup barrier after the table staging: the LDS per wave is its FFT buffer (P and the
+// band gradients reuse it), so 4-wave workgroups fit three to a CU (12 waves) where the slot kernel
+// (138 KB of LDS) fit one 8-wave workgroup. The reflect folds (frame 0 onto samples [1, hop],
+// frame F - 1 onto [2T - 1 - F hop, T - 2]) are added afterwards by k_mel_fold.
+constexpr int kWavesR = 4;
+
+struct RunGeom {
+  int runs_per_item;
+  int64_t runs;  // items * runs_per_item
+};
+
+__host__ __device__ inline int run_gmel_off(int M) { return (M + 1 + 3) & ~3; }
+__host__ __device__ inline int run_wave_floats(int M, int n_mels) {
+  const int a = 2 * (pad(M) + 2), b = run_gmel_off(M) + n_mels;
+  return ((a > b ? a : b) + 3) & ~3;
+}
+
+// the frame's windowed gradient pairs (g[2n], g[2n+1]), n = lane + 64 j, from buf
+template <int LOGN, int KJ>
+__device__ __forceinline__ void frame_pairs(const float* __restrict__ win, const float2* buf, float2 (&gp)[KJ],
+                                            int lane) {
+  constexpr int M = 1 << (LOGN - 1);
+#pragma unroll
+  for (int j = 0; j < KJ; ++j) {
+    const int n = lane + 64 * j;
+    if (M % 64 == 0 || n < M) {
+      const float2 z = buf[pad(n)];
+      gp[j] = make_float2(win[2 * n] * (0.5f * z.x), win[2 * n + 1] * (0.5f * z.y));
+    }
+  }
+}
+
 template <int LOGN, bool STAGE>
-__global__ void __launch_bounds__(64 * kWavesA) k_mel_adj(MelGeom g, const float* __restrict__ wave,
-                                                          const float* __restrict__ gdb,
-                                                          const float* __restrict__ tables,
-                                                          const int* __restrict__ index, float* __restrict__ gwave) {
+__global__ void __launch_bounds__(64 * kWavesR) __attribute__((amdgpu_waves_per_eu(3, 8)))
+    k_mel_adj_run(MelGeom g, RunGeom rg, const float* __restrict__ wave, const float* __restrict__ gdb,
+                  const float* __restrict__ tables, const int* __restrict__ index, float* __restrict__ gwave) {
+  constexpr int N = 1 << LOGN, M = N / 2, KJ = M / 64 > 0 ? M / 64 : 1, KH = KJ / 2 > 0 ? KJ / 2 : 1;
+  extern __shared__ float4 lds_raw[];
+  float* lf = reinterpret_cast<float*>(lds_raw);
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Tabs t = stage_tables<STAGE>(g, N, tables, index, lf, true);
+  float* wbase = lf + (STAGE ? tab_floats(N, g.n_mels, g.nnz, true) : 0) + w * run_wave_floats(M, g.n_mels);
+  float2* buf = reinterpret_cast<float2*>(wbase);
+  float* gmel = wbase + run_gmel_off(M);
+  const int hop = g.hop, F = g.F;
+  const int64_t T = g.T;
+  const int nb = (int)((T + hop - 1) / hop);
+  const int64_t stride = (int64_t)gridDim.x * kWavesR;
+  for (int64_t run = (int64_t)blockIdx.x * kWavesR + w; run < rg.runs; run += stride) {
+    const int64_t it = run / rg.runs_per_item;
+    const int r = (int)(run - it * rg.runs_per_item);
+    const int b0 = (int)((int64_t)r * nb / rg.runs_per_item), b1 = (int)((int64_t)(r + 1) * nb / rg.runs_per_item);
+    const int fe = min(b1, F - 1);
+    const float* x = wave + it * T;
+    const float* gd = gdb + it * (int64_t)F * g.n_mels;
+    float* o = gwave + it * T;
+    const bool vec = ((it * T) & 1) == 0;  // float2 stores stay 8-byte aligned
+    // block b (samples b hop + 2n + e, n = lane + 64 j, j < KH) = a (+ bsec)
+    auto put_block = [&](int b, const float2 (&a)[KH], const float2* bsec) {
+      const int64_t s0 = (int64_t)b * hop;
+#pragma unroll
+      for (int j = 0; j < KH; ++j) {
+        const int n = lane + 64 * j;
+        if (2 * n < hop) {
+          float2 v = a[j];
+          if (bsec) v = make_float2(v.x + bsec[j].x, v.y + bsec[j].y);
+          const int64_t s = s0 + 2 * n;
+          if (vec && s + 1 < T) {
+            *reinterpret_cast<float2*>(o + s) = v;
+          } else {
+            if (s < T) o[s] = v.x;
+            if (s + 1 < T) o[s + 1] = v.y;
+          }
+        }
+      }
+    };
+    FrameIn<LOGN> in;
+    in.fetch(x, T, b0, hop, F, lane);
+    float2 carry[KH];
+    for (int f = b0; f <= fe; ++f) {
+      frame_adjoint_buf<LOGN>(g, t, in, x, f, f < fe ? f + 1 : -1, gd, buf, gmel, lane);
+      float2 gp[KJ];
+      frame_pairs<LOGN, KJ>(t.win, buf, gp, lane);
+      if (f > b0) put_block(f - 1, carry, gp);  // frame f - 1's second half + frame f's first half
+      if constexpr (KJ >= 2) {
+#pragma unroll
+        for (int j = 0; j < KH; ++j) carry[j] = gp[KH + j];
+      } else {  // M <= 64: the second half is lanes M/2 .. M-1
+        carry[0] = make_float2(__shfl(gp[0].x, (lane + M / 2) & 63, 64), __shfl(gp[0].y, (lane + M / 2) & 63, 64));
+      }
+      wave_sync();
+    }
+    if (fe == F - 1 && fe < b1) put_block(fe, carry, nullptr);  // the last block: no next frame
+  }
+}
+
+// The reflect folds, after k_mel_adj_run: wave 2 i recomputes frame 0 of waveform i and adds it
+// onto samples [1, min(hop, T - 1)], wave 2 i + 1 frame F - 1 onto [2T - 1 - F hop, T - 2] (the
+// slot kernel's order: regular frames, then frame 0, then frame F - 1; the two run in sequence
+// inside one wave when the regions overlap, T < 2 hop)
+template <int LOGN, bool STAGE>
+__global__ void __launch_bounds__(64 * kWavesR) __attribute__((amdgpu_waves_per_eu(3, 8)))
+    k_mel_fold(MelGeom g, const float* __restrict__ wave, const float* __restrict__ gdb,
+               const float* __restrict__ tables, const int* __restrict__ index, float* __restrict__ gwave) {
   constexpr int N = 1 << LOGN, M = N / 2;
   extern __shared__ float4 lds_raw[];
   float* lf = reinterpret_cast<float*>(lds_raw);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int BPW = g.blocks_per_wg;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Tabs t = stage_tables<STAGE>(g, N, tables, index, lf, true);
-  float* slots = lf + (STAGE ? tab_floats(N, g.n_mels, g.nnz, true) : 0);  // (BPW + 2) x N
-  float2* bufs = reinterpret_cast<float2*>(slots + (int64_t)(BPW + 2) * N);
-  float2* buf = bufs + w * (pad(M) + 2);
-  float* gmel = reinterpret_cast<float*>(bufs + kWavesA * (pad(M) + 2)) + w * g.n_mels;
-  const int64_t it = blockIdx.x / g.wg_per_item;
-  const int c = (int)(blockIdx.x - it * g.wg_per_item);
+  float* wbase = lf + (STAGE ? tab_floats(N, g.n_mels, g.nnz, true) : 0) + w * run_wave_floats(M, g.n_mels);
+  float2* buf = reinterpret_cast<float2*>(wbase);
+  float* gmel = wbase + run_gmel_off(M);
   const int hop = g.hop, F = g.F;
   const int64_t T = g.T;
-  const int b0 = c * BPW, b1 = b0 + BPW;
-  const int64_t s_lo = (int64_t)b0 * hop, s_hi = min((int64_t)b1 * hop, T);
-  const int f_hi = min(b1, F - 1);
-  const int nat = f_hi - b0 + 1;
-  // the last frame folds back onto [2T - 1 - F hop, T - 2]; a run ending just before it needs it too
   const int64_t r_lo = 2 * T - 1 - (int64_t)F * hop;
-  const bool extra_last = f_hi < F - 1 && s_hi - 1 >= r_lo;
-  const int nframes = nat + (extra_last ? 1 : 0);
+  const bool overlap = r_lo <= hop;  // both folds touch a sample: one wave does both, in order
+  const int64_t q = (int64_t)blockIdx.x * kWavesR + w;
+  if (q >= 2 * g.items) return;
+  const int64_t it = q >> 1;
+  const int side = (int)(q & 1);
+  if (overlap && side) return;
   const float* x = wave + it * T;
   const float* gd = gdb + it * (int64_t)F * g.n_mels;
-  FrameIn<LOGN> in;
-  if (w < nframes) in.fetch(x, T, w < nat ? b0 + w : F - 1, hop, F, lane);
-  for (int i = w; i < nframes; i += kWavesA) {
-    const int f = i < nat ? b0 + i : F - 1;
-    const int in_ = i + kWavesA;
-    const int f_next = in_ < nframes ? (in_ < nat ? b0 + in_ : F - 1) : -1;
-    frame_adjoint<LOGN>(g, t, in, x, f, f_next, gd, buf, gmel, slots + (int64_t)i * N, lane);
-  }
-  __syncthreads();
-  const int last_slot = extra_last ? nat : F - 1 - b0;  // slot of frame F - 1 if held
   float* o = gwave + it * T;
-  for (int64_t s = s_lo + threadIdx.x; s < s_hi; s += blockDim.x) {
-    const int b = (int)(s / hop);
-    const int n = (int)(s - (int64_t)b * hop);
-    float acc = slots[(int64_t)(b - b0) * N + n + hop];  // frame b
-    if (b + 1 <= F - 1) acc += slots[(int64_t)(b + 1 - b0) * N + n];  // frame b + 1
-    if (s >= 1 && s <= hop) acc += slots[hop - s];  // frame 0 (b0 == 0 here), reflected
-    const int64_t se = 2 * (T - 1) - s;
-    if (se >= T && s >= r_lo) acc += slots[(int64_t)last_slot * N + (se - (int64_t)(F - 2) * hop)];
-    o[s] = acc;
+  FrameIn<LOGN> in;
+  for (int k = side; k < (overlap ? 2 : side + 1); ++k) {
+    const int f = k ? F - 1 : 0;
+    in.fetch(x, T, f, hop, F, lane);
+    frame_adjoint_buf<LOGN>(g, t, in, x, f, -1, gd, buf, gmel, lane);
+    auto at = [&](int n) {  // the frame's windowed gradient at sample n of the frame
+      const float2 z = buf[pad(n >> 1)];
+      return t.win[n] * (0.5f * ((n & 1) ? z.y : z.x));
+    };
+    if (k == 0) {
+      for (int64_t s = 1 + lane; s <= min((int64_t)hop, T - 1); s += 64) o[s] += at((int)(hop - s));
+    } else {
+      for (int64_t s = max(r_lo, (int64_t)0) + lane; s <= T - 2; s += 64)
+        o[s] += at((int)(2 * (T - 1) - s - (int64_t)(F - 2) * hop));
+    }
+    wave_sync();
   }
 }
 
@@ -468,19 +559,6 @@ constexpr int kMaxLds = 160 * 1024;
 int lds_fwd(int log_n, int n_mels, int nnz) {
   const int N = 1 << log_n, M = N / 2;
   return (log_n <= 10 ? tab_floats(N, n_mels, nnz, false) * 4 : 0) + kWavesF * (M + (M >> 4) + 2) * 8;
-}
-
-int lds_adj(int log_n, int bpw, int n_mels, int nnz) {
-  const int N = 1 << log_n, M = N / 2;
-  return (log_n <= 10 ? tab_floats(N, n_mels, nnz, true) * 4 : 0) + (bpw + 2) * N * 4 +
-         kWavesA * (M + (M >> 4) + 2) * 8 + kWavesA * n_mels * 4;
-}
-
-// hop-blocks per adjoint workgroup: 15 (16 frames = 2 per wave) when LDS allows, at least 2
-int blocks_per_wg(int log_n, int n_mels, int nnz) {
-  int bpw = 15;
-  while (bpw > 2 && lds_adj(log_n, bpw, n_mels, nnz) > kMaxLds) --bpw;
-  return bpw;
 }
 
 int lds_opt_in_mel(const void* kern, int bytes) {
@@ -530,7 +608,9 @@ extern "C" int wam_melspec(int64_t items, int64_t samples, int n_fft, int n_mels
   int cus = 256;
   {
     int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
   }
   // persistent-ish grid: a few workgroups per CU, each wave streaming frames with one-ahead prefetch
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((frames + kWavesF - 1) / kWavesF, 4 * cus));
@@ -566,24 +646,61 @@ extern "C" int wam_melspec_adjoint(int64_t items, int64_t samples, int n_fft, in
   g.nnz = nnz;
   g.to_db = to_db ? 1 : 0;
   const int nb = (int)((samples + g.hop - 1) / g.hop);
-  g.blocks_per_wg = blocks_per_wg(log_n, n_mels, nnz);
-  g.wg_per_item = (nb + g.blocks_per_wg - 1) / g.blocks_per_wg;
-  const int lds = lds_adj(log_n, g.blocks_per_wg, n_mels, nnz);
-  if (lds > kMaxLds) return WAM_ERR_UNSUPPORTED;
-  if (items * g.wg_per_item > 0x7fffffff) return WAM_ERR_INVALID_ARG;
   hipStream_t st = (hipStream_t)stream;
-  const unsigned grid = (unsigned)(items * g.wg_per_item);
-  WamTimer tm(st, "k_mel_adj", 8.0 * (double)items * samples + 4.0 * (double)items * g.F * n_mels);
+  const int M = n_fft / 2;
+  const int lds = ((log_n <= 10 ? tab_floats(n_fft, n_mels, nnz, true) : 0) + kWavesR * run_wave_floats(M, n_mels)) * 4;
+  if (lds > kMaxLds) return WAM_ERR_UNSUPPORTED;
+  const void* kern = nullptr;
+  const void* kfold = nullptr;
   switch (log_n) {
-#define WAM_MELA(L)                                                                                              \
-  case L:                                                                                                        \
-    if (int rc = lds_opt_in_mel((const void*)k_mel_adj<L, (L <= 10)>, lds)) return rc;                           \
-    hipLaunchKernelGGL((k_mel_adj<L, (L <= 10)>), dim3(grid), dim3(64 * kWavesA), lds, st, g, wave, grad_out, tables, \
-                       index, grad_wave);                                                                        \
+#define WAM_MELR(L)                                     \
+  case L:                                               \
+    kern = (const void*)k_mel_adj_run<L, (L <= 10)>;    \
+    kfold = (const void*)k_mel_fold<L, (L <= 10)>;      \
     break;
-    WAM_MELA(6) WAM_MELA(7) WAM_MELA(8) WAM_MELA(9) WAM_MELA(10) WAM_MELA(11)
-#undef WAM_MELA
+    WAM_MELR(6) WAM_MELR(7) WAM_MELR(8) WAM_MELR(9) WAM_MELR(10) WAM_MELR(11)
+#undef WAM_MELR
     default: return WAM_ERR_UNSUPPORTED;
+  }
+  if (int rc = lds_opt_in_mel(kern, lds)) return rc;
+  if (int rc = lds_opt_in_mel(kfold, lds)) return rc;
+  int dev = 0, cus = 256, per_cu = 1;
+  WAM_HIP_CHECK(hipGetDevice(&dev));
+  WAM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kWavesR, lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  // runs of about 16 hop-blocks (one extra frame each), their count rounded to whole rounds of the
+  // resident waves (the runs cost the same)
+  const int64_t resident = (int64_t)per_cu * cus * kWavesR;
+  const int64_t want = std::max<int64_t>(1, (items * nb + 8 * resident) / (16 * resident)) * resident;
+  RunGeom rg{};
+  rg.runs_per_item = (int)std::max<int64_t>(1, std::min<int64_t>(nb, (want + items / 2) / items));
+  rg.runs = items * rg.runs_per_item;
+  const int64_t wgs = std::min<int64_t>((rg.runs + kWavesR - 1) / kWavesR, (int64_t)per_cu * cus);
+  const unsigned fold_wgs = (unsigned)((2 * items + kWavesR - 1) / kWavesR);
+  {
+    WamTimer tm(st, "k_mel_adj", 8.0 * (double)items * samples + 4.0 * (double)items * g.F * n_mels);
+    switch (log_n) {
+#define WAM_MELR(L)                                                                                       \
+  case L:                                                                                                 \
+    hipLaunchKernelGGL((k_mel_adj_run<L, (L <= 10)>), dim3((unsigned)wgs), dim3(64 * kWavesR), lds, st, g, rg, \
+                       wave, grad_out, tables, index, grad_wave);                                         \
+    break;
+      WAM_MELR(6) WAM_MELR(7) WAM_MELR(8) WAM_MELR(9) WAM_MELR(10) WAM_MELR(11)
+#undef WAM_MELR
+    }
+    WAM_LAUNCH_CHECK();
+  }
+  // the folds: two frames per waveform recomputed, 2 hop samples read and written
+  WamTimer tm(st, "k_mel_fold", 4.0 * (double)items * (2.0 * n_fft + 2.0 * n_mels + 4.0 * g.hop));
+  switch (log_n) {
+#define WAM_MELR(L)                                                                                            \
+  case L:                                                                                                      \
+    hipLaunchKernelGGL((k_mel_fold<L, (L <= 10)>), dim3(fold_wgs), dim3(64 * kWavesR), lds, st, g, wave, grad_out, \
+                       tables, index, grad_wave);                                                              \
+    break;
+    WAM_MELR(6) WAM_MELR(7) WAM_MELR(8) WAM_MELR(9) WAM_MELR(10) WAM_MELR(11)
+#undef WAM_MELR
   }
   WAM_LAUNCH_CHECK();
   return WAM_OK;
