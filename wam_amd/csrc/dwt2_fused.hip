@@ -10,15 +10,15 @@
 // halo is re-read inside a chunk and nothing but the four outputs goes back to HBM. The same
 // kernel is the adjoint (zero padding, reverse(rec) filters) used for the backward pass.
 //
-// Synthesis (k_dwt2_syn): one wave owns 64 coefficient columns and a chunk of coefficient rows.
-// Each lane keeps a ring of the last L/2 coefficient rows of A/H/V/D, combines them vertically
-// (polyphase, two output rows per coefficient row), exchanges the per-column results through a
-// wave-private LDS float4 row and combines horizontally; lanes L/2-1..63 own complete outputs, so
-// a strip produces 130 - L output columns. The IG path scaling alpha is applied on load.
+// Synthesis (k_dwt2_syn): one wave owns 64 coefficient columns and a chunk of coefficient rows and
+// runs the streaming level synthesis shared with the plane-resident kernel (wam_rows::syn_stream:
+// L/2-row register rings, polyphase vertical pass, LDS float4 exchange, horizontal pass; rows
+// fetched 4 ahead, output pairs stored as float2); a strip produces 130 - L output columns. The IG
+// path scaling alpha is applied on load.
 //
 // Waves are independent (no workgroup barriers): 4 waves per 256-thread block, LDS only for the
 // wave-private rows, ordered by the wave's own in-order LDS queue (wave-scope fences).
-#include "kernels.hpp"
+#include "rowtools.hpp"
 
 namespace {
 
@@ -127,10 +127,8 @@ template <int L>
 __global__ void __launch_bounds__(256) k_dwt2_syn(const float* __restrict__ A, const float* __restrict__ Hh,
                                                   const float* __restrict__ Vv, const float* __restrict__ Dd,
                                                   int mh, int mw, float sa, float sd, float* __restrict__ out,
-                                                  int nh, int nw, int p, const float* __restrict__ filt,
-                                                  int nstrips, int nchunks, int RQ, int64_t total_waves) {
-  constexpr int H2 = L / 2;
-  constexpr int OUTQ = 65 - H2;  // coefficient columns completed per strip
+                                                  int nh, int nw, const float* __restrict__ filt, int nstrips,
+                                                  int nchunks, int RQ, int64_t total_waves) {
   __shared__ __attribute__((aligned(16))) float4 xch[4][64];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -142,97 +140,21 @@ __global__ void __launch_bounds__(256) k_dwt2_syn(const float* __restrict__ A, c
   const int64_t t = gw / nstrips;
   const int chunk = (int)(t % nchunks);
   const int64_t plane = t / nchunks;
-
   float rlo[L], rhi[L];
 #pragma unroll
   for (int k = 0; k < L; ++k) {
     rlo[k] = filt[k];
     rhi[k] = filt[L + k];
   }
-  const int qs = p >> 1;  // p is even (p = L - 2)
-  const int c0 = qs + strip * OUTQ - (H2 - 1);
-  const int jj = c0 + lane;
-  const bool colv = jj >= 0 && jj < mw;
-  const int64_t in_plane = (int64_t)mh * mw;
-  const float* pA = A + plane * in_plane;
-  const float* pH = Hh + plane * in_plane;
-  const float* pV = Vv + plane * in_plane;
-  const float* pD = Dd + plane * in_plane;
-  float* po = out + plane * (int64_t)nh * nw;
-  const int qlast = (p + nh - 1) >> 1;
+  constexpr int qs = (L - 2) >> 1;
+  const int qlast = (L - 2 + nh - 1) >> 1;
   const int qbeg = qs + chunk * RQ;
   const int qend = min(qbeg + RQ, qlast + 1);
-  const bool producer = lane >= H2 - 1;
-  const int ucol = 2 * (jj - qs);  // cropped output column of r_col = 0
-
-  float ra[H2], rh_[H2], rv[H2], rd[H2];
-  auto load_row = [&](int q, float& a, float& h, float& v, float& d) {
-    if (colv && q >= 0 && q < mh) {
-      int64_t o = (int64_t)q * mw + jj;
-      a = sa * pA[o];
-      h = sd * pH[o];
-      v = sd * pV[o];
-      d = sd * pD[o];
-    } else {
-      a = h = v = d = 0.f;
-    }
-  };
-#pragma unroll
-  for (int k = 0; k < H2 - 1; ++k) load_row(qbeg - (H2 - 1) + k, ra[k], rh_[k], rv[k], rd[k]);
-  float4* myx = xch[wv];
-  for (int q = qbeg; q < qend; ++q) {
-    load_row(q, ra[H2 - 1], rh_[H2 - 1], rv[H2 - 1], rd[H2 - 1]);
-    // vertical: rows 2q (r=0) and 2q+1 (r=1); ring index H2-1-i'' holds coefficient row q-i''
-    float lo0 = 0.f, lo1 = 0.f, hi0 = 0.f, hi1 = 0.f;
-#pragma unroll
-    for (int i2 = 0; i2 < H2; ++i2) {
-      const int s = H2 - 1 - i2;
-      lo0 = fmaf(rlo[2 * i2], ra[s], lo0);
-      lo0 = fmaf(rhi[2 * i2], rh_[s], lo0);
-      lo1 = fmaf(rlo[2 * i2 + 1], ra[s], lo1);
-      lo1 = fmaf(rhi[2 * i2 + 1], rh_[s], lo1);
-      hi0 = fmaf(rlo[2 * i2], rv[s], hi0);
-      hi0 = fmaf(rhi[2 * i2], rd[s], hi0);
-      hi1 = fmaf(rlo[2 * i2 + 1], rv[s], hi1);
-      hi1 = fmaf(rhi[2 * i2 + 1], rd[s], hi1);
-    }
-    myx[lane] = make_float4(lo0, lo1, hi0, hi1);
-    wave_sync();
-    if (producer) {
-      float o00 = 0.f, o01 = 0.f, o10 = 0.f, o11 = 0.f;  // o[row r][col c]
-#pragma unroll
-      for (int i2 = 0; i2 < H2; ++i2) {
-        float4 n = myx[lane - i2];
-        o00 = fmaf(rlo[2 * i2], n.x, o00);
-        o00 = fmaf(rhi[2 * i2], n.z, o00);
-        o01 = fmaf(rlo[2 * i2 + 1], n.x, o01);
-        o01 = fmaf(rhi[2 * i2 + 1], n.z, o01);
-        o10 = fmaf(rlo[2 * i2], n.y, o10);
-        o10 = fmaf(rhi[2 * i2], n.w, o10);
-        o11 = fmaf(rlo[2 * i2 + 1], n.y, o11);
-        o11 = fmaf(rhi[2 * i2 + 1], n.w, o11);
-      }
-      const int r0 = 2 * (q - qs);  // cropped output row of r = 0
-      if (ucol >= 0) {
-        if (r0 < nh) {
-          if (ucol < nw) po[(int64_t)r0 * nw + ucol] = o00;
-          if (ucol + 1 < nw) po[(int64_t)r0 * nw + ucol + 1] = o01;
-        }
-        if (r0 + 1 < nh) {
-          if (ucol < nw) po[(int64_t)(r0 + 1) * nw + ucol] = o10;
-          if (ucol + 1 < nw) po[(int64_t)(r0 + 1) * nw + ucol + 1] = o11;
-        }
-      }
-    }
-    wave_sync();
-#pragma unroll
-    for (int k = 0; k < H2 - 1; ++k) {
-      ra[k] = ra[k + 1];
-      rh_[k] = rh_[k + 1];
-      rv[k] = rv[k + 1];
-      rd[k] = rd[k + 1];
-    }
-  }
+  const int64_t in_plane = (int64_t)mh * mw;
+  // long filters prefetch 2 rows ahead: 4 would cost the L = 16 kernel 3 waves per SIMD
+  wam_rows::syn_stream<L, (L >= 12 ? 2 : 4)>(A + plane * in_plane, sa, Hh + plane * in_plane, Vv + plane * in_plane, Dd + plane * in_plane,
+                          sd, mh, mw, out + plane * (int64_t)nh * nw, nh, nw, strip, qbeg, qend, xch[wv], rlo, rhi,
+                          lane, (nw & 1) == 0);
 }
 
 constexpr int kTargetWaves = 16384;
@@ -275,7 +197,7 @@ int launch_syn_L(int64_t batch, const float* A, const float* H, const float* V, 
   int64_t blocks = (waves + 3) / 4;
   WamTimer tm(st, "k_dwt2_syn", 4.0 * (double)batch * (4.0 * mh * mw + (double)nh * nw));
   hipLaunchKernelGGL(k_dwt2_syn<L>, dim3((unsigned)blocks), dim3(256), 0, st, A, H, V, D, mh, mw, sa, sd, out, nh, nw,
-                     p, filt, nstrips, nchunks, RQ, waves);
+                     filt, nstrips, nchunks, RQ, waves);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }

@@ -595,7 +595,6 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
 // scheme of k_dwt2_syn, same arithmetic order), coefficient rows are prefetched kSynPF rows ahead
 // with clamped, unconditional loads; only level 0 writes to HBM.
 constexpr int kMaxAlpha = 128;
-constexpr int kSynPF = 4;
 
 struct SynGeom {
   int J;
@@ -612,110 +611,6 @@ struct SynGeom {
 struct SynAlphas {
   float v[kMaxAlpha];
 };
-
-// one level's streaming synthesis for (strip, coefficient rows [qbeg, qend)) of one wave
-template <int L>
-__device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float sa, const float* __restrict__ pH,
-                                           const float* __restrict__ pV, const float* __restrict__ pD, float sd,
-                                           int mh, int mw, float* __restrict__ dst, int oh, int ow, int strip,
-                                           int qbeg, int qend, float4* xch, const float (&rlo)[L],
-                                           const float (&rhi)[L], int lane) {
-  constexpr int p = L - 2;
-  constexpr int H2 = L / 2;
-  constexpr int OUTQ = 65 - H2;
-  constexpr int PF = kSynPF;
-  const int qs = p >> 1;
-  const int jj = qs + strip * OUTQ - (H2 - 1) + lane;
-  const bool colv = jj >= 0 && jj < mw;
-  const int jc = min(max(jj, 0), mw - 1);
-  const bool producer = lane >= H2 - 1;
-  const int ucol = 2 * (jj - qs);
-  // raw fetched rows (a, h, v, d) + validity; scaled / zeroed when they enter the ring
-  float fa[PF], fh[PF], fv[PF], fd[PF];
-  bool fok[PF];
-  auto fetch = [&](int u, int q) {
-    fok[u] = colv && q >= 0 && q < mh;
-    const int o = min(max(q, 0), mh - 1) * mw + jc;
-    fa[u] = pA[o];
-    fh[u] = pH[o];
-    fv[u] = pV[o];
-    fd[u] = pD[o];
-  };
-  float ra[H2], rh[H2], rv[H2], rd[H2];
-#pragma unroll
-  for (int k = 0; k < H2 - 1; ++k) {
-    fetch(0, qbeg - (H2 - 1) + k);
-    ra[k] = fok[0] ? sa * fa[0] : 0.f;
-    rh[k] = fok[0] ? sd * fh[0] : 0.f;
-    rv[k] = fok[0] ? sd * fv[0] : 0.f;
-    rd[k] = fok[0] ? sd * fd[0] : 0.f;
-  }
-#pragma unroll
-  for (int u = 0; u < PF; ++u) fetch(u, qbeg + u);
-  for (int base = qbeg; base < qend; base += PF) {
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      const int q = base + u;
-      ra[H2 - 1] = fok[u] ? sa * fa[u] : 0.f;
-      rh[H2 - 1] = fok[u] ? sd * fh[u] : 0.f;
-      rv[H2 - 1] = fok[u] ? sd * fv[u] : 0.f;
-      rd[H2 - 1] = fok[u] ? sd * fd[u] : 0.f;
-      fetch(u, q + PF);  // past the chunk: clamped, never used
-      float lo0 = 0.f, lo1 = 0.f, hi0 = 0.f, hi1 = 0.f;
-#pragma unroll
-      for (int i2 = 0; i2 < H2; ++i2) {
-        const int sl = H2 - 1 - i2;
-        lo0 = fmaf(rlo[2 * i2], ra[sl], lo0);
-        lo0 = fmaf(rhi[2 * i2], rh[sl], lo0);
-        lo1 = fmaf(rlo[2 * i2 + 1], ra[sl], lo1);
-        lo1 = fmaf(rhi[2 * i2 + 1], rh[sl], lo1);
-        hi0 = fmaf(rlo[2 * i2], rv[sl], hi0);
-        hi0 = fmaf(rhi[2 * i2], rd[sl], hi0);
-        hi1 = fmaf(rlo[2 * i2 + 1], rv[sl], hi1);
-        hi1 = fmaf(rhi[2 * i2 + 1], rd[sl], hi1);
-      }
-      xch[lane] = make_float4(lo0, lo1, hi0, hi1);
-      wsync();
-      if (producer && q < qend) {
-        float o00 = 0.f, o01 = 0.f, o10 = 0.f, o11 = 0.f;
-#pragma unroll
-        for (int i2 = 0; i2 < H2; ++i2) {
-          const float4 n = xch[lane - i2];
-          o00 = fmaf(rlo[2 * i2], n.x, o00);
-          o00 = fmaf(rhi[2 * i2], n.z, o00);
-          o01 = fmaf(rlo[2 * i2 + 1], n.x, o01);
-          o01 = fmaf(rhi[2 * i2 + 1], n.z, o01);
-          o10 = fmaf(rlo[2 * i2], n.y, o10);
-          o10 = fmaf(rhi[2 * i2], n.w, o10);
-          o11 = fmaf(rlo[2 * i2 + 1], n.y, o11);
-          o11 = fmaf(rhi[2 * i2 + 1], n.w, o11);
-        }
-        const int r0 = 2 * (q - qs);
-        if (ucol >= 0 && ucol < ow) {
-          const bool two = ucol + 1 < ow;
-          if (r0 < oh) {
-            float* d0 = dst + (int64_t)r0 * ow + ucol;
-            if (two) *reinterpret_cast<float2*>(d0) = make_float2(o00, o01);
-            else d0[0] = o00;
-          }
-          if (r0 + 1 < oh) {
-            float* d1 = dst + (int64_t)(r0 + 1) * ow + ucol;
-            if (two) *reinterpret_cast<float2*>(d1) = make_float2(o10, o11);
-            else d1[0] = o10;
-          }
-        }
-      }
-      wsync();
-#pragma unroll
-      for (int k = 0; k < H2 - 1; ++k) {
-        ra[k] = ra[k + 1];
-        rh[k] = rh[k + 1];
-        rv[k] = rv[k + 1];
-        rd[k] = rd[k + 1];
-      }
-    }
-  }
-}
 
 // the waves of the workgroup split a level into strips x row chunks
 template <int L>

@@ -131,4 +131,126 @@ __device__ __forceinline__ void hfilter(const float* lds, int j, int p, const fl
   hi = d;
 }
 
+// ------------------------------------------------------------------------------------------------
+// One level's streaming synthesis (waverec2 level) for (strip, coefficient rows [qbeg, qend)) of
+// one wave, shared by the plane-resident synthesis (dwt2_plane.hip) and the per-level kernel
+// (dwt2_fused.hip): every lane keeps a ring of the last L/2 coefficient rows of A/H/V/D (scaled on
+// entry: sa for A, sd for the details -- the IG alpha), combines them vertically (polyphase, two
+// output rows per coefficient row), exchanges the per-column results through the wave's LDS float4
+// row and combines horizontally; lanes L/2-1..63 own complete outputs (a strip yields 130 - L output
+// columns). Coefficient rows are fetched kSynPF rows ahead with clamped, unconditional loads.
+// vec2: output row bases are 8-byte aligned (pairs stored as float2).
+constexpr int kSynPF = 4;
+
+template <int L, int PF = kSynPF>
+__device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float sa, const float* __restrict__ pH,
+                                           const float* __restrict__ pV, const float* __restrict__ pD, float sd,
+                                           int mh, int mw, float* __restrict__ dst, int oh, int ow, int strip,
+                                           int qbeg, int qend, float4* xch, const float (&rlo)[L],
+                                           const float (&rhi)[L], int lane, bool vec2 = true) {
+  constexpr int p = L - 2;
+  constexpr int H2 = L / 2;
+  constexpr int OUTQ = 65 - H2;
+  const int qs = p >> 1;
+  const int jj = qs + strip * OUTQ - (H2 - 1) + lane;
+  const bool colv = jj >= 0 && jj < mw;
+  const int jc = min(max(jj, 0), mw - 1);
+  const bool producer = lane >= H2 - 1;
+  const int ucol = 2 * (jj - qs);
+  // raw fetched rows (a, h, v, d) + validity; scaled / zeroed when they enter the ring
+  float fa[PF], fh[PF], fv[PF], fd[PF];
+  bool fok[PF];
+  auto fetch = [&](int u, int q) {
+    fok[u] = colv && q >= 0 && q < mh;
+    const int o = min(max(q, 0), mh - 1) * mw + jc;
+    fa[u] = pA[o];
+    fh[u] = pH[o];
+    fv[u] = pV[o];
+    fd[u] = pD[o];
+  };
+  float ra[H2], rh[H2], rv[H2], rd[H2];
+#pragma unroll
+  for (int k = 0; k < H2 - 1; ++k) {
+    fetch(0, qbeg - (H2 - 1) + k);
+    ra[k] = fok[0] ? sa * fa[0] : 0.f;
+    rh[k] = fok[0] ? sd * fh[0] : 0.f;
+    rv[k] = fok[0] ? sd * fv[0] : 0.f;
+    rd[k] = fok[0] ? sd * fd[0] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < PF; ++u) fetch(u, qbeg + u);
+  for (int base = qbeg; base < qend; base += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int q = base + u;
+      ra[H2 - 1] = fok[u] ? sa * fa[u] : 0.f;
+      rh[H2 - 1] = fok[u] ? sd * fh[u] : 0.f;
+      rv[H2 - 1] = fok[u] ? sd * fv[u] : 0.f;
+      rd[H2 - 1] = fok[u] ? sd * fd[u] : 0.f;
+      fetch(u, q + PF);  // past the chunk: clamped, never used
+      float lo0 = 0.f, lo1 = 0.f, hi0 = 0.f, hi1 = 0.f;
+#pragma unroll
+      for (int i2 = 0; i2 < H2; ++i2) {
+        const int sl = H2 - 1 - i2;
+        lo0 = fmaf(rlo[2 * i2], ra[sl], lo0);
+        lo0 = fmaf(rhi[2 * i2], rh[sl], lo0);
+        lo1 = fmaf(rlo[2 * i2 + 1], ra[sl], lo1);
+        lo1 = fmaf(rhi[2 * i2 + 1], rh[sl], lo1);
+        hi0 = fmaf(rlo[2 * i2], rv[sl], hi0);
+        hi0 = fmaf(rhi[2 * i2], rd[sl], hi0);
+        hi1 = fmaf(rlo[2 * i2 + 1], rv[sl], hi1);
+        hi1 = fmaf(rhi[2 * i2 + 1], rd[sl], hi1);
+      }
+      xch[lane] = make_float4(lo0, lo1, hi0, hi1);
+      wsync();
+      if (producer && q < qend) {
+        float o00 = 0.f, o01 = 0.f, o10 = 0.f, o11 = 0.f;
+#pragma unroll
+        for (int i2 = 0; i2 < H2; ++i2) {
+          const float4 n = xch[lane - i2];
+          o00 = fmaf(rlo[2 * i2], n.x, o00);
+          o00 = fmaf(rhi[2 * i2], n.z, o00);
+          o01 = fmaf(rlo[2 * i2 + 1], n.x, o01);
+          o01 = fmaf(rhi[2 * i2 + 1], n.z, o01);
+          o10 = fmaf(rlo[2 * i2], n.y, o10);
+          o10 = fmaf(rhi[2 * i2], n.w, o10);
+          o11 = fmaf(rlo[2 * i2 + 1], n.y, o11);
+          o11 = fmaf(rhi[2 * i2 + 1], n.w, o11);
+        }
+        const int r0 = 2 * (q - qs);
+        if (ucol >= 0 && ucol < ow) {
+          const bool two = ucol + 1 < ow, pair = two && vec2;
+          if (r0 < oh) {
+            float* d0 = dst + (int64_t)r0 * ow + ucol;
+            if (pair) {
+              *reinterpret_cast<float2*>(d0) = make_float2(o00, o01);
+            } else {
+              d0[0] = o00;
+              if (two) d0[1] = o01;
+            }
+          }
+          if (r0 + 1 < oh) {
+            float* d1 = dst + (int64_t)(r0 + 1) * ow + ucol;
+            if (pair) {
+              *reinterpret_cast<float2*>(d1) = make_float2(o10, o11);
+            } else {
+              d1[0] = o10;
+              if (two) d1[1] = o11;
+            }
+          }
+        }
+      }
+      wsync();
+#pragma unroll
+      for (int k = 0; k < H2 - 1; ++k) {
+        ra[k] = ra[k + 1];
+        rh[k] = rh[k + 1];
+        rv[k] = rv[k + 1];
+        rd[k] = rd[k + 1];
+      }
+    }
+  }
+}
+
+
 }  // namespace wam_rows
