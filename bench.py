@@ -546,6 +546,40 @@ def _cmp(a, b, what):
             "top10_iou": round(_top_iou(a, b), 4), "items": int(a.shape[0])}
 
 
+def _main_map(o):
+    """the attribution map of a call's output (1D: (mel maps, coefficient maps) -> the mel maps)"""
+    return np.asarray(o[0] if isinstance(o, tuple) else o)
+
+
+def parity_extras(wl, dev, args, ex, x, y, cpu_ref):
+    """c3 / c4 / c5: the GPU path (fp32 model as is, the reference's numpy noise for SmoothGrad) vs
+    the CPU reference path's own output (cpu_baseline) on the same items, samples / path steps and
+    weights; where the headline model runs in bf16, the headline map vs that fp32 map too."""
+    n_img, n_s, ref = cpu_ref
+    yy = y[:n_img] if isinstance(y, list) else y
+    smooth = wl.kw.get("method", "smooth") == "smooth"
+    ex32 = build_explainer(wl, dev, args, model_dtype="fp32", optimize=False, noise="numpy" if smooth else None)
+    ex32.n_samples = n_s
+    got = ex32(x[:n_img], yy)
+    par = {"gpu_fp32_vs_cpu_reference": _cmp(_main_map(got), _main_map(ref),
+                                             "GPU (fp32 model as is%s) vs the CPU reference path (cpu_baseline's own "
+                                             "output), same items / weights / %s" % (
+                                                 ", numpy noise" if smooth else "",
+                                                 "noise" if smooth else "path steps"))}
+    par["gpu_fp32_vs_cpu_reference"]["n_samples"] = n_s
+    if (args.model_dtype or wl.model_dtype) == "bf16":
+        hd = build_explainer(wl, dev, args, noise="numpy" if smooth else None)
+        hd.n_samples = n_s
+        par["bf16_headline_vs_fp32"] = _cmp(_main_map(hd(x[:n_img], yy)), _main_map(got),
+                                            "headline model (bf16%s) vs fp32 model as is, same items and %s: model "
+                                            "precision only" % (", BN-folded" if wl.dim == 2 else "",
+                                                                "noise" if smooth else "path steps"))
+        del hd
+    del ex32
+    torch.cuda.empty_cache()
+    return par
+
+
 def c2_extras(wl, dev, args, ex, x, y, cpu_ref):
     """Parity numbers on the headline configuration, variant throughputs and ceilings."""
     import wam_amd
@@ -727,6 +761,7 @@ def main():
             "what": "timed calls replay the reference's legacy numpy noise stream from the device (drawn once per "
                     "seed / shape / batch, scaled per call, bit-exact); cold_call_ms = one call after clearing it"}
     if wl.dim == 2:
+        log(".scales host copy")
         # .scales (lib/wam_2D.py:413,457): the reprojection kernel runs inside every timed call;
         # its float64 host copy is made on first access -- its cost, outside the timed region:
         torch.cuda.synchronize(dev)
@@ -738,7 +773,9 @@ def main():
                     "device -> host float64 copy on first access of ex.scales, not in the timed region"}
         del sc
     if world > 1:
+        log("collectives timing")
         secondary["collectives"] = collectives_timing(wl, dev, world, axis)
+        log("weak scaling: each rank its own %d-item batch" % wl.n)
         exw = build_explainer(wl, dev, args, dist_on=False)  # each rank its own batch, no collective
         dtw, _, _ = timed(lambda: exw(xd, y), 2, 1, world, dev)
         secondary["weak_scaling"] = {"value": round(wl.n * 2 * world / dtw, 3), "ms_per_step": round(dtw / 2 * 1e3, 2),
@@ -757,6 +794,9 @@ def main():
         n_img, n_s, ref = cpu_ref
         extras["parity"] = {"gpu_vs_cpu_reference": _cmp(out[:n_img], ref, "GPU vs CPU reference path, same input, "
                                                                             "weights and numpy noise")}
+    elif cpu_ref is not None and args.extras == "auto":
+        log("%s extras: parity" % wl.name)
+        extras["parity"] = parity_extras(wl, dev, args, ex, xd, y, cpu_ref)
 
     model_dtype = args.model_dtype or wl.model_dtype
     total = wl.n * args.steps

@@ -306,7 +306,7 @@ int wam_visualize3d(int64_t items, int size, int levels, const float* cube, floa
  * when to_db, and the gradient torch autograd takes through it).
  * wave [items, samples] float32 (samples > n_fft / 2); out / grad_out [items, F, n_mels] with
  * F = samples / (n_fft / 2) + 1 (the reference's [N, 1, F, n_mels] stack); n_fft a power of two
- * in [64, 4096] (WAM_ERR_UNSUPPORTED otherwise).
+ * in [64, 2048], n_mels <= 256 (WAM_ERR_UNSUPPORTED otherwise).
  * tables (float, device): window[n_fft] | twiddle[2 n_fft] (cos, sin of -2 pi m / n_fft) |
  *   band_w[nnz] | bin_w[nnz];
  * index (int32, device): band_ptr[n_mels + 1] | band_bin[nnz] | bin_ptr[n_fft / 2 + 2] |

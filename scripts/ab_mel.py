@@ -1,5 +1,6 @@
-"""A/B of the mel adjoint kernels in one process each: WAM_MEL_ADJ_SLOTS=1 selects the slot kernel.
-usage: python scripts/ab_mel.py <out.npz>  -> saves adjoints of several shapes + c3 timing."""
+"""A/B of the mel kernels, one library per process (WAM_LIB_PATH=build/exp/<variant>.so for the
+other arm). usage: python scripts/ab_mel.py <out.npz>  -> saves forwards and adjoints of several
+shapes (compare with scripts/ab_mel_cmp.py) and prints the c3-group times."""
 import os
 import sys
 
@@ -18,17 +19,20 @@ for i, (n, t, m, sr, b) in enumerate(CASES):
     x = torch.randn(b, t, generator=g).cuda()
     go = torch.randn(b, t // (n // 2) + 1, m, generator=g).cuda()
     out["c%d" % i] = M.mel_adjoint(x, go, n, sr, m).cpu().numpy()
+    out["f%d" % i] = M.mel_forward(x, n, sr, m).cpu().numpy()
 x = torch.randn(1280, 80000, device="cuda")
 go = torch.randn(1280, 157, 128, device="cuda")
-for _ in range(2):
-    M.mel_adjoint(x, go, 1024, 16000, 128)
-torch.cuda.synchronize()
-s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-s.record()
-for _ in range(10):
-    M.mel_adjoint(x, go, 1024, 16000, 128)
-e.record()
-torch.cuda.synchronize()
-print("%s mel_adjoint c3 group (1280 x 80000): %.1f us" % ("slots" if os.environ.get("WAM_MEL_ADJ_SLOTS") else "runs",
-                                                           1e3 * s.elapsed_time(e) / 10))
+tag = os.environ.get("WAM_LIB_PATH", "in-tree libwam_hip.so")
+for name, fn in (("mel_forward", lambda: M.mel_forward(x, 1024, 16000, 128)),
+                 ("mel_adjoint", lambda: M.mel_adjoint(x, go, 1024, 16000, 128))):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(10):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    print("%s: %s c3 group (1280 x 80000): %.1f us" % (tag, name, 1e3 * s.elapsed_time(e) / 10))
 np.savez(sys.argv[1], **out)

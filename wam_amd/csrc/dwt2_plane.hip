@@ -24,6 +24,7 @@
 // XCD (L2); for noisy analysis the logical order is sample-fastest, so the S noise samples of one
 // clean plane run back to back on one XCD and its rows are read from HBM about once.
 #include <atomic>
+#include <cstdlib>
 
 #include "rowtools.hpp"
 
@@ -51,6 +52,7 @@ struct PlaneGeom {
   int rowlds;                       // floats per wave-private row
   int llcap;                        // floats of LDS buffer A (LL_1, LL_3, ...)
   int sample_fast;                  // noisy analysis: logical order sample-fastest (1) or plane-fastest (0)
+  int xcd_order;                    // workgroup ids through the XCD-aware swizzle (1) or as issued (0)
   int coop;                         // level 1 as the cooperative row stream (COOP kernels)
 };
 
@@ -92,7 +94,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
   // ---- logical workgroup: bijective XCD swizzle (consecutive logical ids share an XCD)
   const int64_t nwg = gridDim.x, bid = blockIdx.x;
   const int64_t q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-  const int64_t lwg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int64_t lwg = g.xcd_order ? (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8 : bid;
   if (lwg >= n_items) return;  // never taken (grid == n_items); keeps the barrier count uniform
 
   // the wave index is wave-uniform: readfirstlane puts it (and every row index, ring slot and
@@ -760,7 +762,14 @@ PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items
   g.maps_item = p->band_off[p->nbands];
   lds_floats(p, nw0, g.rowlds, g.llcap, noisy);
   g.coop = coop_ok(p, nw0, noisy);
-  g.sample_fast = 1;
+  // WAM_PLANE_ORDER (A/B): 0 plane-fastest, 1 sample-fastest through the XCD swizzle (default),
+  // 2 sample-fastest as issued (a plane's samples spread over the XCDs)
+  static const int order = [] {
+    const char* e = getenv("WAM_PLANE_ORDER");
+    return e ? atoi(e) : 1;
+  }();
+  g.sample_fast = order != 0;
+  g.xcd_order = order != 2;
   return g;
 }
 

@@ -245,35 +245,43 @@ __global__ void __launch_bounds__(256) k_frame_accumulate_coef(int64_t groups, i
                                                                const int32_t* __restrict__ cband,
                                                                const float* __restrict__ maps,
                                                                const float* __restrict__ band_max, int n_bands,
-                                                               int normalize, double* __restrict__ frame) {
-  const int64_t total = group_items * maps_item_len;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t n = t / maps_item_len;
-    const int64_t k = t - n * maps_item_len;
+                                                               int normalize, int64_t items_per_thread,
+                                                               double* __restrict__ frame) {
+  // thread per (coefficient k, run of items_per_thread items): the mosaic tables (8 B per
+  // coefficient, several MB at 512^2, beyond an XCD's L2) are read once per run of items instead of
+  // once per item
+  const int64_t mstride = group_items * maps_item_len;
+  const int64_t runs = (group_items + items_per_thread - 1) / items_per_thread;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < runs * maps_item_len;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / maps_item_len;
+    const int64_t k = t - r * maps_item_len;
     const int32_t d = dst[k];
     if (d < 0) continue;
     const int32_t b = cband[k];
-    double* fp = frame + n * frame_len + d;
-    double acc = *fp;
-    const float* mp = maps + t;
-    const int64_t mstride = group_items * maps_item_len;
-    int64_t s = 0;
-    for (; s + 8 <= groups; s += 8) {
-      float v[8], m[8];
+    const int64_t n1 = min(group_items, (r + 1) * items_per_thread);
+    for (int64_t n = r * items_per_thread; n < n1; ++n) {
+      double* fp = frame + n * frame_len + d;
+      double acc = *fp;
+      const float* mp = maps + n * maps_item_len + k;
+      int64_t s = 0;
+      for (; s + 8 <= groups; s += 8) {
+        float v[8], m[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        v[u] = mp[(s + u) * mstride];
-        m[u] = normalize ? band_max[(s + u) * n_bands + b] : 1.f;
+        for (int u = 0; u < 8; ++u) {
+          v[u] = mp[(s + u) * mstride];
+          m[u] = normalize ? band_max[(s + u) * n_bands + b] : 1.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += (double)(normalize ? v[u] / m[u] : v[u]);
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc += (double)(normalize ? v[u] / m[u] : v[u]);
+      for (; s < groups; ++s) {
+        float v = mp[s * mstride];
+        if (normalize) v = v / band_max[s * n_bands + b];
+        acc += (double)v;
+      }
+      *fp = acc;
     }
-    for (; s < groups; ++s) {
-      float v = mp[s * mstride];
-      if (normalize) v = v / band_max[s * n_bands + b];
-      acc += (double)v;
-    }
-    *fp = acc;
   }
 }
 
@@ -634,8 +642,13 @@ int wam_frame_accumulate_coef(int64_t groups, int64_t group_items, int64_t maps_
   if (work == 0 || groups == 0) return WAM_OK;
   WamTimer tm((hipStream_t)stream, "k_frame_accumulate_coef",
               4.0 * (double)groups * group_items * frame_len + 16.0 * group_items * frame_len + 8.0 * frame_len);
-  hipLaunchKernelGGL(k_frame_accumulate_coef, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, groups,
-                     group_items, maps_item_len, frame_len, dst, cband, maps, band_max, n_bands, normalize, frame);
+  // about a million threads, each a run of items of one coefficient
+  int64_t ipt = work / (int64_t(1) << 20);
+  ipt = ipt < 1 ? 1 : (ipt > group_items ? group_items : ipt);
+  const int64_t threads = (group_items + ipt - 1) / ipt * maps_item_len;
+  hipLaunchKernelGGL(k_frame_accumulate_coef, dim3(wam_grid(threads, 256)), dim3(256), 0, (hipStream_t)stream, groups,
+                     group_items, maps_item_len, frame_len, dst, cband, maps, band_max, n_bands, normalize, ipt,
+                     frame);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }

@@ -152,6 +152,58 @@ __device__ __forceinline__ void fft_stage(float2* buf, const float2* __restrict_
   wave_sync();
 }
 
+// Register-fed / register-draining forms of a stage for the M = 512 transforms (three radix-8
+// stages of 64 butterflies, one per lane): stage 0 reads elements lane + 64 r, which are the
+// frame's samples a lane already holds (IN = 1) or the Hermitian pack of the adjoint spectrum
+// computed on the load from A (IN = 2: Z''[k] = (A_k + conj A_(M-k)) + i (A_k - conj A_(M-k))
+// e^(+2 pi i k / N)); the last stage writes elements lane + 64 r, which stay in registers
+// (OUT = 1). Same arithmetic as fft_stage, fewer LDS round trips.
+template <int LOGN, int ST, int S, int IN, bool OUT>
+__device__ __forceinline__ void fft_stage_io(float2* buf, const float2* __restrict__ tw, int lane,
+                                             const float2* vin, float2* vout) {
+  constexpr int LOGM = LOGN - 1, M = 1 << LOGM;
+  constexpr int LR = Plan<LOGM>::log_radix(ST), R = 1 << LR;
+  constexpr int LNS = Plan<LOGM>::log_ns(ST), Ns = 1 << LNS;
+  constexpr int B = M / R;
+  static_assert(R == 8 && B == 64, "the register forms are for 512-point stages");
+  static_assert(IN == 0 || ST == 0, "register input: first stage only");
+  static_assert(!OUT || LNS + LR == LOGM, "register output: last stage only");
+  const int j = lane, k = j & (Ns - 1);
+  float2 v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    float2 x;
+    if constexpr (IN == 1) {
+      x = vin[r];
+    } else if constexpr (IN == 2) {
+      const int q = j + r * B;
+      const float2 ak = buf[pad(q)], ac = cconj(buf[pad(M - q)]);
+      const float2 d = cmul(csub(ak, ac), cconj(tw[q]));
+      const float2 sm = cadd(ak, ac);
+      x = make_float2(sm.x - d.y, sm.y + d.x);
+    } else {
+      x = buf[pad(j + r * B)];
+    }
+    if (Ns > 1 && r > 0) {
+      float2 t = tw[(r * k) << (LOGN - LNS - LR)];
+      if (S > 0) t = cconj(t);
+      x = cmul(x, t);
+    }
+    v[r] = x;
+  }
+  dft8<S>(v);
+  if constexpr (OUT) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) vout[r] = v[r];  // element j + r Ns = j + 64 r
+  } else {
+    wave_sync();
+    const int idx = ((j >> LNS) << (LNS + LR)) + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) buf[pad(idx + r * Ns)] = v[r];
+    wave_sync();
+  }
+}
+
 template <int LOGN, int ST, int S>
 __device__ __forceinline__ void fft_stages(float2* buf, const float2* __restrict__ tw, int lane) {
   if constexpr (ST < Plan<LOGN - 1>::stages) {
@@ -274,9 +326,8 @@ __device__ __forceinline__ float2 unpack_bin(const float2* buf, const float2* tw
 
 // FFT of the stored frame, then P[k] = |X[k]|^2 into buf (as floats, k <= M); X kept if asked
 template <int LOGN, bool KEEP>
-__device__ __forceinline__ void frame_power(const Tabs& t, float2* buf, float2* X, int lane) {
+__device__ __forceinline__ void frame_unpack_power(const Tabs& t, float2* buf, float2* X, int lane) {
   constexpr int M = 1 << (LOGN - 1), KI = M / 64 + 1;
-  fft_stages<LOGN, 0, -1>(buf, t.tw, lane);
   float p[KI];
 #pragma unroll
   for (int i = 0; i < KI; ++i) {
@@ -295,11 +346,25 @@ __device__ __forceinline__ void frame_power(const Tabs& t, float2* buf, float2* 
   wave_sync();
 }
 
+template <int LOGN, bool KEEP>
+__device__ __forceinline__ void frame_power(const Tabs& t, float2* buf, float2* X, int lane) {
+  fft_stages<LOGN, 0, -1>(buf, t.tw, lane);
+  frame_unpack_power<LOGN, KEEP>(t, buf, X, lane);
+}
+
 __device__ __forceinline__ float band_sum(const Tabs& t, const float* P, int m) {
   float acc = 0.f;
-  const int e1 = t.band_ptr[m + 1];
+  const int e0 = t.band_ptr[m], e1 = t.band_ptr[m + 1];
+  if (e1 > e0 && t.band_bin[e1 - 1] - t.band_bin[e0] == e1 - 1 - e0) {
+    // a triangular band's bins are consecutive: the P and weight loads do not wait on an index
+    // load (same terms, same order)
+    const float* pb = P + (t.band_bin[e0] - e0);
 #pragma unroll 4
-  for (int e = t.band_ptr[m]; e < e1; ++e) acc = fmaf(P[t.band_bin[e]], t.band_w[e], acc);
+    for (int e = e0; e < e1; ++e) acc = fmaf(pb[e], t.band_w[e], acc);
+    return acc;
+  }
+#pragma unroll 4
+  for (int e = e0; e < e1; ++e) acc = fmaf(P[t.band_bin[e]], t.band_w[e], acc);
   return acc;
 }
 
@@ -318,11 +383,24 @@ __global__ void __launch_bounds__(64 * kWavesF) k_mel_fwd(MelGeom g, const float
   FrameIn<LOGN> in;
   if (q < frames) in.fetch(wave + (q / g.F) * g.T, g.T, (int)(q % g.F), g.hop, g.F, lane);
   for (; q < frames; q += stride) {
-    in.store(t.win, buf, lane);
     const int64_t qn = q + stride;
-    if (qn < frames) in.fetch(wave + (qn / g.F) * g.T, g.T, (int)(qn % g.F), g.hop, g.F, lane);
-    wave_sync();
-    frame_power<LOGN, false>(t, buf, nullptr, lane);
+    if constexpr (LOGN == 10) {  // 512-point transform: the first stage fed from registers
+      float2 z0[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int n = lane + 64 * i;
+        z0[i] = make_float2(in.a[i] * t.win[2 * n], in.b[i] * t.win[2 * n + 1]);
+      }
+      fft_stage_io<LOGN, 0, -1, 1, false>(buf, t.tw, lane, z0, nullptr);
+      if (qn < frames) in.fetch(wave + (qn / g.F) * g.T, g.T, (int)(qn % g.F), g.hop, g.F, lane);
+      fft_stages<LOGN, 1, -1>(buf, t.tw, lane);
+      frame_unpack_power<LOGN, false>(t, buf, nullptr, lane);
+    } else {
+      in.store(t.win, buf, lane);
+      if (qn < frames) in.fetch(wave + (qn / g.F) * g.T, g.T, (int)(qn % g.F), g.hop, g.F, lane);
+      wave_sync();
+      frame_power<LOGN, false>(t, buf, nullptr, lane);
+    }
     const float* P = reinterpret_cast<const float*>(buf);
     float* o = out + q * g.n_mels;
     for (int m = lane; m < g.n_mels; m += 64) {
@@ -339,18 +417,34 @@ __global__ void __launch_bounds__(64 * kWavesF) k_mel_fwd(MelGeom g, const float
 template <int LOGN>
 __device__ __forceinline__ void frame_adjoint_buf(const MelGeom& g, const Tabs& t, FrameIn<LOGN>& in,
                                                   const float* __restrict__ x, int f, int f_next,
-                                                  const float* __restrict__ gdb, float2* buf, float* gmel, int lane) {
+                                                  const float* __restrict__ gdb, float2* buf, float* gmel, int lane,
+                                                  float2* zout = nullptr) {
   constexpr int M = 1 << (LOGN - 1), KI = M / 64 + 1;
   constexpr int kMelRegs = 4;  // bands lane + 64 j, j < 4, held in registers (n_mels <= 256)
-  in.store(t.win, buf, lane);
-  if (f_next >= 0) in.fetch(x, g.T, f_next, g.hop, g.F, lane);
+  constexpr bool FAST = LOGN == 10;  // 512-point transforms: register-fed first / last stages
   float gq[kMelRegs];
   const float* gf = gdb + (int64_t)f * g.n_mels;
 #pragma unroll
   for (int j = 0; j < kMelRegs; ++j) gq[j] = lane + 64 * j < g.n_mels ? gf[lane + 64 * j] : 0.f;
-  wave_sync();
   float2 X[KI];
-  frame_power<LOGN, true>(t, buf, X, lane);
+  if constexpr (FAST) {
+    // stage 0 straight from the windowed samples in registers (no store + reload of the frame)
+    float2 z0[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int n = lane + 64 * i;
+      z0[i] = make_float2(in.a[i] * t.win[2 * n], in.b[i] * t.win[2 * n + 1]);
+    }
+    fft_stage_io<LOGN, 0, -1, 1, false>(buf, t.tw, lane, z0, nullptr);
+    if (f_next >= 0) in.fetch(x, g.T, f_next, g.hop, g.F, lane);
+    fft_stages<LOGN, 1, -1>(buf, t.tw, lane);
+    frame_unpack_power<LOGN, true>(t, buf, X, lane);
+  } else {
+    in.store(t.win, buf, lane);
+    if (f_next >= 0) in.fetch(x, g.T, f_next, g.hop, g.F, lane);
+    wave_sync();
+    frame_power<LOGN, true>(t, buf, X, lane);
+  }
   const float* P = reinterpret_cast<const float*>(buf);
   // d db / d mel: mul(10) -> log10 -> clamp(min=1e-10), in torch's order
 #pragma unroll
@@ -385,6 +479,15 @@ __device__ __forceinline__ void frame_adjoint_buf(const MelGeom& g, const Tabs& 
   for (int i = 0; i < KI; ++i)
     if (lane + 64 * i <= M) buf[pad(lane + 64 * i)] = A[i];
   wave_sync();
+  if constexpr (FAST) {
+    // the Hermitian pack computed on the first inverse stage's load; the last stage's output
+    // (z[lane + 64 r]) stays in registers or goes back to buf
+    fft_stage_io<LOGN, 0, 1, 2, false>(buf, t.tw, lane, nullptr, nullptr);
+    fft_stage_io<LOGN, 1, 1, 0, false>(buf, t.tw, lane, nullptr, nullptr);
+    if (zout) fft_stage_io<LOGN, 2, 1, 0, true>(buf, t.tw, lane, nullptr, zout);
+    else fft_stage_io<LOGN, 2, 1, 0, false>(buf, t.tw, lane, nullptr, nullptr);
+    return;
+  }
   // Z''[k] = (A_k + conj A_{M-k}) + i (A_k - conj A_{M-k}) e^{+2 pi i k/N},  k < M
   float2 Zp[KI];
 #pragma unroll
@@ -491,9 +594,19 @@ __global__ void __launch_bounds__(64 * kWavesR) __attribute__((amdgpu_waves_per_
     in.fetch(x, T, b0, hop, F, lane);
     float2 carry[KH];
     for (int f = b0; f <= fe; ++f) {
-      frame_adjoint_buf<LOGN>(g, t, in, x, f, f < fe ? f + 1 : -1, gd, buf, gmel, lane);
       float2 gp[KJ];
-      frame_pairs<LOGN, KJ>(t.win, buf, gp, lane);
+      if constexpr (LOGN == 10) {  // the last inverse stage's output straight from registers
+        float2 z[8];
+        frame_adjoint_buf<LOGN>(g, t, in, x, f, f < fe ? f + 1 : -1, gd, buf, gmel, lane, z);
+#pragma unroll
+        for (int j = 0; j < KJ; ++j) {
+          const int n = lane + 64 * j;
+          gp[j] = make_float2(t.win[2 * n] * (0.5f * z[j].x), t.win[2 * n + 1] * (0.5f * z[j].y));
+        }
+      } else {
+        frame_adjoint_buf<LOGN>(g, t, in, x, f, f < fe ? f + 1 : -1, gd, buf, gmel, lane);
+        frame_pairs<LOGN, KJ>(t.win, buf, gp, lane);
+      }
       if (f > b0) put_block(f - 1, carry, gp);  // frame f - 1's second half + frame f's first half
       if constexpr (KJ >= 2) {
 #pragma unroll
