@@ -642,8 +642,10 @@ int wam_frame_accumulate_coef(int64_t groups, int64_t group_items, int64_t maps_
   if (work == 0 || groups == 0) return WAM_OK;
   WamTimer tm((hipStream_t)stream, "k_frame_accumulate_coef",
               4.0 * (double)groups * group_items * frame_len + 16.0 * group_items * frame_len + 8.0 * frame_len);
-  // about a million threads, each a run of items of one coefficient
-  int64_t ipt = work / (int64_t(1) << 20);
+  // mosaic tables beyond ~2 MB (8 B per coefficient; 512^2 planes) would be re-read from HBM per
+  // item: about a million threads then, each a run of items of one coefficient; small tables stay
+  // in L2 and every (item, coefficient) gets its own thread
+  int64_t ipt = maps_item_len * 8 > (int64_t(2) << 20) ? work / (int64_t(1) << 20) : 1;
   ipt = ipt < 1 ? 1 : (ipt > group_items ? group_items : ipt);
   const int64_t threads = (group_items + ipt - 1) / ipt * maps_item_len;
   hipLaunchKernelGGL(k_frame_accumulate_coef, dim3(wam_grid(threads, 256)), dim3(256), 0, (hipStream_t)stream, groups,
