@@ -30,6 +30,9 @@ namespace {
 
 using namespace wam_rows;
 
+template <int L>
+constexpr bool kRolledPrologue = L >= 12;
+
 // ------------------------------------------------------------------------------------------------
 template <int L, int CPL, int VEC, int MAXV, bool NOISE>
 __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, int nh, int nw, int64_t in_plane,
@@ -103,21 +106,33 @@ __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, 
     wsync();
   };
 
+  // Long filters (kRolledPrologue) fill the ring by (L - 2) / 2 warm-up passes of the row loop
+  // itself (outputs not stored): unrolled, the prologue's L - 2 row passes are scheduled together
+  // and hold ~4x the loop's registers at L = 16 (AGPR-resident LDS reads: 1 wave per SIMD instead
+  // of 4). Short filters keep the unrolled prologue (the warm-up passes' vertical filters cost
+  // 4-7 % at L = 8, profiles/r03i_kbench_c2_rows_rolled_ab.log).
   float rl[CPL][L], rh[CPL][L];
   fetch(f[0], nzv[0], er0);
+  if constexpr (kRolledPrologue<L>) {
 #pragma unroll
-  for (int k = 0; k < L - 2; ++k) {
-    fetch(f[(k + 1) & 1], nzv[(k + 1) & 1], er0 + k + 1);
-    float lo[CPL], hi[CPL];
-    process(f[k & 1], nzv[k & 1], lo, hi);
+    for (int c = 0; c < CPL; ++c)
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      rl[c][k] = lo[c];
-      rh[c][k] = hi[c];
+      for (int k = 0; k < L; ++k) rl[c][k] = rh[c][k] = 0.f;
+  } else {
+#pragma unroll
+    for (int k = 0; k < L - 2; ++k) {
+      fetch(f[(k + 1) & 1], nzv[(k + 1) & 1], er0 + k + 1);
+      float lo[CPL], hi[CPL];
+      process(f[k & 1], nzv[k & 1], lo, hi);
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        rl[c][k] = lo[c];
+        rh[c][k] = hi[c];
+      }
     }
   }
   // invariant: f[0] holds ext row er0 + 2*(i - i0) + L - 2
-  for (int i = i0; i < i1; ++i) {
+  for (int i = i0 - (kRolledPrologue<L> ? (L - 2) / 2 : 0); i < i1; ++i) {
     const int er = er0 + 2 * (i - i0) + L - 2;
     fetch(f[1], nzv[1], er + 1);
     float lo[CPL], hi[CPL];
@@ -145,7 +160,7 @@ __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, 
         v = fmaf(flo[k], rh[c][k], v);
         d = fmaf(fhi[k], rh[c][k], d);
       }
-      if (j < mw) {
+      if (j < mw && (!kRolledPrologue<L> || i >= i0)) {
         const int64_t o = plane * out_plane + (int64_t)i * mw + j;
         oa[o] = a;
         oh[o] = h;
@@ -256,26 +271,37 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
     wsync();
   };
 
+  // long filters: ring filled by (L - 2) / 2 warm-up passes of the row loop (see k_ana_rows)
   float rl[C][CPL][L], rh[C][CPL][L];
   fetch(f[0], er0);
-#pragma unroll
-  for (int k = 0; k < L - 2; ++k) {
-    fetch(f[(k + 1) & 1], er0 + k + 1);
-    float lo[C][CPL], hi[C][CPL];
-    process(f[k & 1], lo, hi);
+  if constexpr (kRolledPrologue<L>) {
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int q = 0; q < CPL; ++q) {
-        rl[c][q][k] = lo[c][q];
-        rh[c][q][k] = hi[c][q];
-      }
+      for (int q = 0; q < CPL; ++q)
+#pragma unroll
+        for (int k = 0; k < L; ++k) rl[c][q][k] = rh[c][q][k] = 0.f;
+  } else {
+#pragma unroll
+    for (int k = 0; k < L - 2; ++k) {
+      fetch(f[(k + 1) & 1], er0 + k + 1);
+      float lo[C][CPL], hi[C][CPL];
+      process(f[k & 1], lo, hi);
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) {
+          rl[c][q][k] = lo[c][q];
+          rh[c][q][k] = hi[c][q];
+        }
+    }
   }
   float mx_h = 0.f, mx_v = 0.f, mx_d = 0.f, mx_a = 0.f;
   const bool last = ma.off_a >= 0;
   float* mrow = ma.maps + img * ma.maps_item;
-  for (int i = i0; i < i1; ++i) {
+  for (int i = i0 - (kRolledPrologue<L> ? (L - 2) / 2 : 0); i < i1; ++i) {
     const int er = er0 + 2 * (i - i0) + L - 2;
+    const bool on = !kRolledPrologue<L> || i >= i0;
     fetch(f[1], er + 1);
     float lo[C][CPL], hi[C][CPL];
     process(f[0], lo, hi);
@@ -309,7 +335,7 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
           v = fmaf(flo[k], rh[c][q][k], v);
           d = fmaf(fhi[k], rh[c][q][k], d);
         }
-        if (jv[q]) {
+        if (jv[q] && on) {
           const int64_t plane = img * C + c;
           if (!last) ll_out[plane * out_plane + o] = a;
           if (ma.full) {  // band-major: band b starts at full_items * off_b
@@ -330,7 +356,7 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
           rh[c][q][k] = rh[c][q][k + 2];
         }
       }
-      if (jv[q]) {
+      if (jv[q] && on) {
         const float mh_ = fabsf(sh / (float)C), mv_ = fabsf(sv / (float)C), md_ = fabsf(sd / (float)C);
         mrow[ma.off_h + o] = mh_;
         mrow[ma.off_v + o] = mv_;
@@ -413,7 +439,9 @@ int dispatch_ana_cpl(int64_t batch, const float* in, int nh, int nw, int mh, int
 template <int L>
 int dispatch_ana(int64_t batch, const float* in, int nh, int nw, int mh, int mw, int mode, const float* filt,
                  float* oa, float* oh, float* ov, float* od, const WamNoise* nz, hipStream_t st) {
-  if (mw > 64) return dispatch_ana_cpl<L, 2>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
+  // long filters: one column per lane (4 waves per SIMD at L = 16; two columns measured 157 vs
+  // 116 us at c4 level 1, profiles/r03i_kbench_c4_rows_rolled_ab.log)
+  if (mw > 64 && L < 12) return dispatch_ana_cpl<L, 2>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
   return dispatch_ana_cpl<L, 1>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
 }
 
