@@ -151,6 +151,22 @@ def test_alpha_scaling_matches_scaled_coefficients(wam):
         assert torch.equal(out[i], ref)
 
 
+@pytest.mark.parametrize("wav,shape,J", [("db4", (224, 224), 3), ("sym8", (100, 130), 2), ("haar", (64, 66), 4)])
+def test_alpha_groups_row_synthesis(wam, wav, shape, J):
+    """Row-kernel plans synthesise the IG alphas in groups (one launch per level per group, the
+    details read once per group): 11 alphas (several groups, a partial last one) equal the
+    single-alpha synthesis of the pre-scaled coefficients bit for bit."""
+    p = wam.get_plan(2, shape, J, wav, "reflect", "cuda", flags=wam.PLAN_NO_PLANE)
+    torch.manual_seed(5)
+    B = 5
+    c = torch.randn(B * p.coeff_numel, device="cuda")
+    alphas = np.linspace(0, 1, 11)
+    out = p.waverec(c, B, alphas=alphas)
+    assert out.shape == (11, B) + p.rec_shape
+    for i, a in enumerate(alphas):
+        assert torch.equal(out[i], p.waverec(c * float(np.float32(a)), B)[0]), i
+
+
 def test_transforms_api_autograd(wam):
     """wam_amd.waverec2 backward == the oracle's autograd through ptwt's conv_transpose."""
     import wam_amd
@@ -211,6 +227,23 @@ def test_fused_2d_paths_agree(wam, wav, shape, J, mode):
     ar, ac, ag = rows.adjoint(g), col.adjoint(g), gen.adjoint(g)
     assert torch.equal(ar, ac)
     assert (ar - ag).abs().max().item() <= 1e-5 * ag.abs().max().item()
+
+
+@pytest.mark.parametrize("wav,shape,J,mode", [("db5", (70, 90), 2, "reflect"), ("db6", (64, 130), 3, "symmetric"),
+                                              ("db7", (100, 77), 2, "zero"), ("sym8", (150, 150), 3, "reflect"),
+                                              ("db9", (61, 95), 2, "constant"), ("db10", (128, 40), 1, "reflect")])
+def test_row_synthesis_matches_generic(wam, wav, shape, J, mode):
+    """Per-level row synthesis (k_dwt2_syn; long filters on packed FMAs over a static register
+    ring with lcm(L/2, prefetch) rows per iteration, odd L/2 included) vs the per-axis synthesis,
+    with IG alphas in groups."""
+    torch.manual_seed(8)
+    B = 4
+    rows = wam.get_plan(2, shape, J, wav, mode, "cuda", flags=wam.PLAN_NO_PLANE)
+    gen = wam.get_plan(2, shape, J, wav, mode, "cuda", generic=True)
+    c = gen.wavedec(torch.randn((B,) + shape, device="cuda"))
+    al = [0.0, 0.3, 0.7, 1.0, 0.5, 0.9]
+    a, g = rows.waverec(c, B, alphas=al), gen.waverec(c, B, alphas=al)
+    assert (a - g).abs().max().item() <= 1e-5 * g.abs().max().item()
 
 
 @pytest.mark.parametrize("wav,J", [("db4", 3), ("haar", 3), ("sym8", 2)])

@@ -124,9 +124,8 @@ __global__ void __launch_bounds__(256) k_dwt2_ana(const float* __restrict__ in, 
 }
 
 template <int L>
-__global__ void __launch_bounds__(256) k_dwt2_syn(const float* __restrict__ A, const float* __restrict__ Hh,
-                                                  const float* __restrict__ Vv, const float* __restrict__ Dd,
-                                                  int mh, int mw, float sa, float sd, float* __restrict__ out,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L <= 16 ? 4 : 3, 8))) k_dwt2_syn(const float* __restrict__ Hh, const float* __restrict__ Vv,
+                                                  const float* __restrict__ Dd, int mh, int mw, SynBatch sb,
                                                   int nh, int nw, const float* __restrict__ filt, int nstrips,
                                                   int nchunks, int RQ, int64_t total_waves) {
   __shared__ __attribute__((aligned(16))) float4 xch[4][64];
@@ -134,12 +133,19 @@ __global__ void __launch_bounds__(256) k_dwt2_syn(const float* __restrict__ A, c
   const int wv = threadIdx.x >> 6;
   const int64_t gw = wam_xcd_block(blockIdx.x, gridDim.x) * 4 + wv;
   if (gw >= total_waves) return;
-  // strip fastest: the strips of one (plane, row chunk) -- which fetch the same source rows --
-  // are waves of one workgroup (one CU, one XCD L2) instead of landing on different XCDs
+  // strip fastest, then alpha: the strips of one (plane, row chunk) -- which fetch the same source
+  // rows -- and the alphas of it -- which fetch the same detail rows -- are waves of one or two
+  // neighbouring workgroups (one XCD L2, close in time), so the details come from HBM once per
+  // launch rather than once per alpha
   const int strip = (int)(gw % nstrips);
-  const int64_t t = gw / nstrips;
+  int64_t t = gw / nstrips;
+  const int ai = __builtin_amdgcn_readfirstlane((int)(t % sb.na));  // wave-uniform: kernarg index
+  t /= sb.na;
   const int chunk = (int)(t % nchunks);
   const int64_t plane = t / nchunks;
+  const float* __restrict__ A = sb.a[ai];
+  float* __restrict__ out = sb.out[ai];
+  const float sa = sb.sa[ai], sd = sb.sd[ai];
   float rlo[L], rhi[L];
 #pragma unroll
   for (int k = 0; k < L; ++k) {
@@ -180,13 +186,13 @@ int launch_ana_L(int64_t batch, const float* in, int nh, int nw, int mh, int mw,
 }
 
 template <int L>
-int launch_syn_L(int64_t batch, const float* A, const float* H, const float* V, const float* D, int mh, int mw, float sa,
-                 float sd, float* out, int nh, int nw, int p, const float* filt, hipStream_t st) {
+int launch_syn_L(int64_t batch, const float* H, const float* V, const float* D, int mh, int mw, const SynBatch& sb,
+                 int nh, int nw, int p, const float* filt, hipStream_t st) {
   constexpr int OUTQ = 65 - L / 2;
   int qcols = (nw + 1) / 2;
   int nstrips = (qcols + OUTQ - 1) / OUTQ;
   int nq = (nh + 1) / 2;
-  int64_t base = batch * nstrips;
+  int64_t base = batch * nstrips * sb.na;
   int64_t want = (kTargetWaves + base - 1) / base;
   int maxchunks = (nq + 3) / 4;
   int nchunks = (int)(want < 1 ? 1 : (want > maxchunks ? maxchunks : want));
@@ -195,9 +201,10 @@ int launch_syn_L(int64_t batch, const float* A, const float* H, const float* V, 
   nchunks = (nq + RQ - 1) / RQ;
   int64_t waves = base * nchunks;
   int64_t blocks = (waves + 3) / 4;
-  WamTimer tm(st, "k_dwt2_syn", 4.0 * (double)batch * (4.0 * mh * mw + (double)nh * nw));
-  hipLaunchKernelGGL(k_dwt2_syn<L>, dim3((unsigned)blocks), dim3(256), 0, st, A, H, V, D, mh, mw, sa, sd, out, nh, nw,
-                     filt, nstrips, nchunks, RQ, waves);
+  // algorithmic bytes: per alpha its LL in and its output, the three detail bands once
+  WamTimer tm(st, "k_dwt2_syn", 4.0 * (double)batch * (sb.na * ((double)mh * mw + (double)nh * nw) + 3.0 * mh * mw));
+  hipLaunchKernelGGL(k_dwt2_syn<L>, dim3((unsigned)blocks), dim3(256), 0, st, H, V, D, mh, mw, sb, nh, nw, filt,
+                     nstrips, nchunks, RQ, waves);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }
@@ -225,15 +232,15 @@ int launch_dwt2_analysis_fused(const wam_plan* p, int64_t batch, const float* in
 #undef WAM_ANA_CASE
 }
 
-int launch_dwt2_synthesis_fused(const wam_plan* p, int64_t batch, int level, const float* a_in, float a_scale,
-                                const float* const* sub, float d_scale, float* out, hipStream_t st) {
+int launch_dwt2_synthesis_fused(const wam_plan* p, int64_t batch, int level, const SynBatch& sb,
+                                const float* const* sub, hipStream_t st) {
+  if (sb.na < 1 || sb.na > kSynMaxAlpha) return WAM_ERR_INVALID_ARG;
   const float* filt = p->d_filt + WAM_F_SYN_LO * p->L;
   int mh = (int)p->lout[level][0], mw = (int)p->lout[level][1];
   int nh = (int)(2 * mh - 2 + p->L - 2 * p->pad - p->extra[level][0]);
   int nw = (int)(2 * mw - 2 + p->L - 2 * p->pad - p->extra[level][1]);
-#define WAM_SYN_CASE(LL)                                                                                       \
-  case LL: return launch_syn_L<LL>(batch, a_in, sub[0], sub[1], sub[2], mh, mw, a_scale, d_scale, out, nh, nw, \
-                                   p->pad, filt, st);
+#define WAM_SYN_CASE(LL) \
+  case LL: return launch_syn_L<LL>(batch, sub[0], sub[1], sub[2], mh, mw, sb, nh, nw, p->pad, filt, st);
   switch (p->L) {
     WAM_SYN_CASE(2) WAM_SYN_CASE(4) WAM_SYN_CASE(6) WAM_SYN_CASE(8) WAM_SYN_CASE(10)
     WAM_SYN_CASE(12) WAM_SYN_CASE(14) WAM_SYN_CASE(16) WAM_SYN_CASE(18) WAM_SYN_CASE(20)

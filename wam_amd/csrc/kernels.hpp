@@ -23,8 +23,20 @@ bool dwt2_fused_supported(const wam_plan* p);
 int launch_dwt2_analysis_fused(const wam_plan* p, int64_t batch, const float* in, const int64_t* in_dims,
                                const int64_t* out_dims, int mode, int fset, float* out_a, float* const* sub,
                                hipStream_t st);
-int launch_dwt2_synthesis_fused(const wam_plan* p, int64_t batch, int level, const float* a_in, float a_scale,
-                                const float* const* sub, float d_scale, float* out, hipStream_t st);
+// One synthesis level for up to kSynMaxAlpha IG alphas in one launch: alpha i reads its LL from
+// a[i] (scaled by sa[i]) and the shared detail bands (scaled by sd[i]) and writes out[i].
+constexpr int kSynMaxAlpha = 8;
+// alphas whose intermediate LL planes the plan workspace holds at once (2D row-synthesis plans)
+constexpr int kSynWsAlpha = 4;
+struct SynBatch {
+  const float* a[kSynMaxAlpha];
+  float* out[kSynMaxAlpha];
+  float sa[kSynMaxAlpha];
+  float sd[kSynMaxAlpha];
+  int na;
+};
+int launch_dwt2_synthesis_fused(const wam_plan* p, int64_t batch, int level, const SynBatch& sb,
+                                const float* const* sub, hipStream_t st);
 
 #include "timing.hpp"
 

@@ -192,6 +192,13 @@ int sub_of_key(int nd, int key) {
 
 }  // namespace
 
+// 2D plans whose waverec runs the per-level row synthesis (k_dwt2_syn) rather than the
+// plane-resident kernel: their IG alphas are synthesised kSynWsAlpha per level launch
+static bool syn_rows_alpha_batched(const wam_plan* p) {
+  return p->ndim == 2 && !(p->flags & WAM_PLAN_GENERIC) && dwt2_fused_supported(p) &&
+         ((p->flags & (WAM_PLAN_NO_ROWS | WAM_PLAN_NO_PLANE)) || !dwt2_plane_syn_supported(p));
+}
+
 extern "C" int64_t wam_plan_workspace_bytes(const wam_plan* p, int64_t batch) {
   if (!p || batch < 0) return -1;
   int nd = p->ndim;
@@ -216,6 +223,8 @@ extern "C" int64_t wam_plan_workspace_bytes(const wam_plan* p, int64_t batch) {
   int64_t tmp_s = generic_syn_tmp(p, batch);
   int64_t a_side = 2 * ll + tmp_a;
   int64_t s_side = 2 * rec_ll + tmp_s;
+  // row-synthesis 2D plans: the LL ping-pong of kSynWsAlpha alphas per level launch
+  if (syn_rows_alpha_batched(p) && 2 * kSynWsAlpha * rec_ll > s_side) s_side = 2 * kSynWsAlpha * rec_ll;
   int64_t elems = a_side > s_side ? a_side : s_side;
   return (elems + 64) * (int64_t)sizeof(float);
 }
@@ -504,6 +513,32 @@ int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const flo
     if (v > rec_ll) rec_ll = v;
   }
   float* w = (float*)ws;
+  if (nd == 2 && !(p->flags & WAM_PLAN_GENERIC) && dwt2_fused_supported(p)) {
+    // alphas in groups: one launch per level per group, each level's detail bands read once per
+    // group; the group's intermediate LL planes ping-pong between two workspace sets
+    const int64_t ws_elems = wam_plan_workspace_bytes(p, batch) / (int64_t)sizeof(float) - 64;
+    int64_t g = rec_ll > 0 ? ws_elems / (2 * rec_ll) : kSynMaxAlpha;
+    const int G = (int)(g < 1 ? 1 : (g > kSynMaxAlpha ? kSynMaxAlpha : g));
+    for (int a0 = 0; a0 < n_alpha; a0 += G) {
+      SynBatch sb{};
+      sb.na = n_alpha - a0 < G ? n_alpha - a0 : G;
+      for (int c = 0; c < p->levels; ++c) {
+        const int l = p->levels - 1 - c;
+        float* sub[7];
+        band_ptrs(p, batch, (float*)coeffs, l, sub);
+        for (int i = 0; i < sb.na; ++i) {
+          const float s = alpha ? alpha[a0 + i] : 1.0f;
+          sb.a[i] = c == 0 ? coeffs : w + (int64_t)(((c - 1) & 1) * G + i) * rec_ll;  // band 0 = A_J
+          sb.sa[i] = c == 0 ? s : 1.0f;
+          sb.sd[i] = s;
+          sb.out[i] = l == 0 ? out + (int64_t)(a0 + i) * batch * out_item : w + (int64_t)((c & 1) * G + i) * rec_ll;
+        }
+        int rc = launch_dwt2_synthesis_fused(p, batch, l, sb, sub, st);
+        if (rc) return rc;
+      }
+    }
+    return WAM_OK;
+  }
   float* abuf[2] = {w, w + rec_ll};
   float* tmp = w + 2 * rec_ll;
   for (int ai = 0; ai < n_alpha; ++ai) {
@@ -515,12 +550,7 @@ int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const flo
       float* sub[7];
       band_ptrs(p, batch, (float*)coeffs, l, sub);
       float* dst = (l == 0) ? out + (int64_t)ai * batch * out_item : abuf[c & 1];
-      int rc;
-      if (nd == 2 && !(p->flags & WAM_PLAN_GENERIC) && dwt2_fused_supported(p)) {
-        rc = launch_dwt2_synthesis_fused(p, batch, l, a_cur, a_scale, sub, s, dst, st);
-      } else {
-        rc = generic_synthesis_level(p, batch, l, a_cur, a_scale, sub, s, dst, tmp, st);
-      }
+      int rc = generic_synthesis_level(p, batch, l, a_cur, a_scale, sub, s, dst, tmp, st);
       if (rc) return rc;
       a_cur = dst;
       a_scale = 1.0f;

@@ -142,7 +142,25 @@ __device__ __forceinline__ void hfilter(const float* lds, int j, int p, const fl
 // vec2: output row bases are 8-byte aligned (pairs stored as float2).
 constexpr int kSynPF = 4;
 
-template <int L, int PF = kSynPF>
+constexpr int syn_gcd(int a, int b) { return b == 0 ? a : syn_gcd(b, a % b); }
+constexpr int syn_lcm(int a, int b) { return a / syn_gcd(a, b) * b; }
+
+// acc += w * (x, x): one v_pk_fma_f32 (PK) or two scalar fmas -- the same sums either way
+template <bool PK, class F2>
+__device__ __forceinline__ void syn_fma2(F2& acc, F2 w, float x) {
+  if constexpr (PK) {
+    acc = __builtin_elementwise_fma(w, F2{x, x}, acc);
+  } else {
+    acc.x = fmaf(w.x, x, acc.x);
+    acc.y = fmaf(w.y, x, acc.y);
+  }
+}
+
+// PK (long filters, where the level synthesis is VALU-bound): packed fp32 FMAs over a static
+// register ring, lcm(H2, PF) rows per iteration (sym8 at 512^2: 444 -> 353 us per 2-alpha finest
+// level). Short filters keep scalar chains and a shifted ring: the memory-bound plane synthesis
+// measured 447 vs 439 us in the static-ring form (profiles/r03j_kbench_syn_ab.log)
+template <int L, int PF = kSynPF, bool PK = (L >= 12)>
 __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float sa, const float* __restrict__ pH,
                                            const float* __restrict__ pV, const float* __restrict__ pD, float sd,
                                            int mh, int mw, float* __restrict__ dst, int oh, int ow, int strip,
@@ -168,85 +186,170 @@ __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float s
     fv[u] = pV[o];
     fd[u] = pD[o];
   };
-  float ra[H2], rh[H2], rv[H2], rd[H2];
-#pragma unroll
-  for (int k = 0; k < H2 - 1; ++k) {
-    fetch(0, qbeg - (H2 - 1) + k);
-    ra[k] = fok[0] ? sa * fa[0] : 0.f;
-    rh[k] = fok[0] ? sd * fh[0] : 0.f;
-    rv[k] = fok[0] ? sd * fv[0] : 0.f;
-    rd[k] = fok[0] ? sd * fd[0] : 0.f;
-  }
-#pragma unroll
-  for (int u = 0; u < PF; ++u) fetch(u, qbeg + u);
-  for (int base = qbeg; base < qend; base += PF) {
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      const int q = base + u;
-      ra[H2 - 1] = fok[u] ? sa * fa[u] : 0.f;
-      rh[H2 - 1] = fok[u] ? sd * fh[u] : 0.f;
-      rv[H2 - 1] = fok[u] ? sd * fv[u] : 0.f;
-      rd[H2 - 1] = fok[u] ? sd * fd[u] : 0.f;
-      fetch(u, q + PF);  // past the chunk: clamped, never used
-      float lo0 = 0.f, lo1 = 0.f, hi0 = 0.f, hi1 = 0.f;
-#pragma unroll
-      for (int i2 = 0; i2 < H2; ++i2) {
-        const int sl = H2 - 1 - i2;
-        lo0 = fmaf(rlo[2 * i2], ra[sl], lo0);
-        lo0 = fmaf(rhi[2 * i2], rh[sl], lo0);
-        lo1 = fmaf(rlo[2 * i2 + 1], ra[sl], lo1);
-        lo1 = fmaf(rhi[2 * i2 + 1], rh[sl], lo1);
-        hi0 = fmaf(rlo[2 * i2], rv[sl], hi0);
-        hi0 = fmaf(rhi[2 * i2], rd[sl], hi0);
-        hi1 = fmaf(rlo[2 * i2 + 1], rv[sl], hi1);
-        hi1 = fmaf(rhi[2 * i2 + 1], rd[sl], hi1);
-      }
-      xch[lane] = make_float4(lo0, lo1, hi0, hi1);
-      wsync();
-      if (producer && q < qend) {
-        float o00 = 0.f, o01 = 0.f, o10 = 0.f, o11 = 0.f;
-#pragma unroll
+  if constexpr (PK) {
+    // filter pairs (taps 2 i2, 2 i2 + 1): the two outputs of a phase pair as one (packed) chain
+    // pair, every output keeping the scalar chain's tap order (same sums)
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 flo2[H2], fhi2[H2];
+  #pragma unroll
+    for (int i2 = 0; i2 < H2; ++i2) {
+      flo2[i2] = f2{rlo[2 * i2], rlo[2 * i2 + 1]};
+      fhi2[i2] = f2{rhi[2 * i2], rhi[2 * i2 + 1]};
+    }
+    // ring of the last H2 coefficient rows in static slots: row qbeg - (H2 - 1) + k in slot k mod H2
+    float ra[H2], rh[H2], rv[H2], rd[H2];
+  #pragma unroll
+    for (int k = 0; k < H2 - 1; ++k) {
+      fetch(0, qbeg - (H2 - 1) + k);
+      ra[k] = fok[0] ? sa * fa[0] : 0.f;
+      rh[k] = fok[0] ? sd * fh[0] : 0.f;
+      rv[k] = fok[0] ? sd * fv[0] : 0.f;
+      rd[k] = fok[0] ? sd * fd[0] : 0.f;
+    }
+  #pragma unroll
+    for (int u = 0; u < PF; ++u) fetch(u, qbeg + u);
+    // rows per iteration lcm(H2, PF): ring slots and fetch buffers static across iterations
+    constexpr int GR = syn_lcm(H2, PF);
+    for (int base = qbeg; base < qend; base += GR) {
+  #pragma unroll
+      for (int u = 0; u < GR; ++u) {
+        const int q = base + u;
+        if (q >= qend) break;  // uniform
+        const int uf = u % PF;
+        const int ns = (H2 - 1 + u) % H2;  // slot of row q
+        ra[ns] = fok[uf] ? sa * fa[uf] : 0.f;
+        rh[ns] = fok[uf] ? sd * fh[uf] : 0.f;
+        rv[ns] = fok[uf] ? sd * fv[uf] : 0.f;
+        rd[ns] = fok[uf] ? sd * fd[uf] : 0.f;
+        fetch(uf, q + PF);  // past the chunk: clamped, never used
+        f2 lo = {0.f, 0.f}, hi = {0.f, 0.f};  // (lo0, lo1), (hi0, hi1)
+  #pragma unroll
         for (int i2 = 0; i2 < H2; ++i2) {
-          const float4 n = xch[lane - i2];
-          o00 = fmaf(rlo[2 * i2], n.x, o00);
-          o00 = fmaf(rhi[2 * i2], n.z, o00);
-          o01 = fmaf(rlo[2 * i2 + 1], n.x, o01);
-          o01 = fmaf(rhi[2 * i2 + 1], n.z, o01);
-          o10 = fmaf(rlo[2 * i2], n.y, o10);
-          o10 = fmaf(rhi[2 * i2], n.w, o10);
-          o11 = fmaf(rlo[2 * i2 + 1], n.y, o11);
-          o11 = fmaf(rhi[2 * i2 + 1], n.w, o11);
+          const int sl = (ns - i2 + H2) % H2;  // row q - i2
+          syn_fma2<PK>(lo, flo2[i2], ra[sl]);
+          syn_fma2<PK>(lo, fhi2[i2], rh[sl]);
+          syn_fma2<PK>(hi, flo2[i2], rv[sl]);
+          syn_fma2<PK>(hi, fhi2[i2], rd[sl]);
         }
-        const int r0 = 2 * (q - qs);
-        if (ucol >= 0 && ucol < ow) {
-          const bool two = ucol + 1 < ow, pair = two && vec2;
-          if (r0 < oh) {
-            float* d0 = dst + (int64_t)r0 * ow + ucol;
-            if (pair) {
-              *reinterpret_cast<float2*>(d0) = make_float2(o00, o01);
-            } else {
-              d0[0] = o00;
-              if (two) d0[1] = o01;
+        xch[lane] = make_float4(lo.x, lo.y, hi.x, hi.y);
+        wsync();
+        if (producer) {
+          f2 o0 = {0.f, 0.f}, o1 = {0.f, 0.f};  // (o00, o01), (o10, o11)
+  #pragma unroll
+          for (int i2 = 0; i2 < H2; ++i2) {
+            const float4 n = xch[lane - i2];
+            syn_fma2<PK>(o0, flo2[i2], n.x);
+            syn_fma2<PK>(o0, fhi2[i2], n.z);
+            syn_fma2<PK>(o1, flo2[i2], n.y);
+            syn_fma2<PK>(o1, fhi2[i2], n.w);
+          }
+          const int r0 = 2 * (q - qs);
+          if (ucol >= 0 && ucol < ow) {
+            const bool two = ucol + 1 < ow, pair = two && vec2;
+            if (r0 < oh) {
+              float* d0 = dst + (int64_t)r0 * ow + ucol;
+              if (pair) {
+                *reinterpret_cast<float2*>(d0) = make_float2(o0.x, o0.y);
+              } else {
+                d0[0] = o0.x;
+                if (two) d0[1] = o0.y;
+              }
+            }
+            if (r0 + 1 < oh) {
+              float* d1 = dst + (int64_t)(r0 + 1) * ow + ucol;
+              if (pair) {
+                *reinterpret_cast<float2*>(d1) = make_float2(o1.x, o1.y);
+              } else {
+                d1[0] = o1.x;
+                if (two) d1[1] = o1.y;
+              }
             }
           }
-          if (r0 + 1 < oh) {
-            float* d1 = dst + (int64_t)(r0 + 1) * ow + ucol;
-            if (pair) {
-              *reinterpret_cast<float2*>(d1) = make_float2(o10, o11);
-            } else {
-              d1[0] = o10;
-              if (two) d1[1] = o11;
-            }
-          }
         }
+        wsync();
       }
-      wsync();
-#pragma unroll
-      for (int k = 0; k < H2 - 1; ++k) {
-        ra[k] = ra[k + 1];
-        rh[k] = rh[k + 1];
-        rv[k] = rv[k + 1];
-        rd[k] = rd[k + 1];
+    }
+  } else {  // short filters: scalar chains, ring shifted by register moves
+    float ra[H2], rh[H2], rv[H2], rd[H2];
+  #pragma unroll
+    for (int k = 0; k < H2 - 1; ++k) {
+      fetch(0, qbeg - (H2 - 1) + k);
+      ra[k] = fok[0] ? sa * fa[0] : 0.f;
+      rh[k] = fok[0] ? sd * fh[0] : 0.f;
+      rv[k] = fok[0] ? sd * fv[0] : 0.f;
+      rd[k] = fok[0] ? sd * fd[0] : 0.f;
+    }
+  #pragma unroll
+    for (int u = 0; u < PF; ++u) fetch(u, qbeg + u);
+    for (int base = qbeg; base < qend; base += PF) {
+  #pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int q = base + u;
+        ra[H2 - 1] = fok[u] ? sa * fa[u] : 0.f;
+        rh[H2 - 1] = fok[u] ? sd * fh[u] : 0.f;
+        rv[H2 - 1] = fok[u] ? sd * fv[u] : 0.f;
+        rd[H2 - 1] = fok[u] ? sd * fd[u] : 0.f;
+        fetch(u, q + PF);  // past the chunk: clamped, never used
+        float lo0 = 0.f, lo1 = 0.f, hi0 = 0.f, hi1 = 0.f;
+  #pragma unroll
+        for (int i2 = 0; i2 < H2; ++i2) {
+          const int sl = H2 - 1 - i2;
+          lo0 = fmaf(rlo[2 * i2], ra[sl], lo0);
+          lo0 = fmaf(rhi[2 * i2], rh[sl], lo0);
+          lo1 = fmaf(rlo[2 * i2 + 1], ra[sl], lo1);
+          lo1 = fmaf(rhi[2 * i2 + 1], rh[sl], lo1);
+          hi0 = fmaf(rlo[2 * i2], rv[sl], hi0);
+          hi0 = fmaf(rhi[2 * i2], rd[sl], hi0);
+          hi1 = fmaf(rlo[2 * i2 + 1], rv[sl], hi1);
+          hi1 = fmaf(rhi[2 * i2 + 1], rd[sl], hi1);
+        }
+        xch[lane] = make_float4(lo0, lo1, hi0, hi1);
+        wsync();
+        if (producer && q < qend) {
+          float o00 = 0.f, o01 = 0.f, o10 = 0.f, o11 = 0.f;
+  #pragma unroll
+          for (int i2 = 0; i2 < H2; ++i2) {
+            const float4 n = xch[lane - i2];
+            o00 = fmaf(rlo[2 * i2], n.x, o00);
+            o00 = fmaf(rhi[2 * i2], n.z, o00);
+            o01 = fmaf(rlo[2 * i2 + 1], n.x, o01);
+            o01 = fmaf(rhi[2 * i2 + 1], n.z, o01);
+            o10 = fmaf(rlo[2 * i2], n.y, o10);
+            o10 = fmaf(rhi[2 * i2], n.w, o10);
+            o11 = fmaf(rlo[2 * i2 + 1], n.y, o11);
+            o11 = fmaf(rhi[2 * i2 + 1], n.w, o11);
+          }
+          const int r0 = 2 * (q - qs);
+          if (ucol >= 0 && ucol < ow) {
+            const bool two = ucol + 1 < ow, pair = two && vec2;
+            if (r0 < oh) {
+              float* d0 = dst + (int64_t)r0 * ow + ucol;
+              if (pair) {
+                *reinterpret_cast<float2*>(d0) = make_float2(o00, o01);
+              } else {
+                d0[0] = o00;
+                if (two) d0[1] = o01;
+              }
+            }
+            if (r0 + 1 < oh) {
+              float* d1 = dst + (int64_t)(r0 + 1) * ow + ucol;
+              if (pair) {
+                *reinterpret_cast<float2*>(d1) = make_float2(o10, o11);
+              } else {
+                d1[0] = o10;
+                if (two) d1[1] = o11;
+              }
+            }
+          }
+        }
+        wsync();
+  #pragma unroll
+        for (int k = 0; k < H2 - 1; ++k) {
+          ra[k] = ra[k + 1];
+          rh[k] = rh[k + 1];
+          rv[k] = rv[k + 1];
+          rd[k] = rd[k + 1];
+        }
       }
     }
   }
