@@ -32,6 +32,55 @@ using namespace wam_rows;
 
 template <int L>
 constexpr bool kRolledPrologue = L >= 12;
+// long filters also run their tap chains as packed (lo, hi) / (a, h) / (v, d) pairs (same sums)
+template <int L>
+constexpr bool kPackedTaps = L >= 12;
+
+template <int L>
+__device__ __forceinline__ void tap_pairs(const float (&flo)[L], const float (&fhi)[L], wam_f2 (&fp)[L]) {
+#pragma unroll
+  for (int k = 0; k < L; ++k) fp[k] = wam_f2{flo[k], fhi[k]};
+}
+
+// vertical filter of one column's ring: a = sum flo rl, h = sum fhi rl, v = sum flo rh, d = sum fhi rh
+template <int L>
+__device__ __forceinline__ void vfilter(const float (&flo)[L], const float (&fhi)[L], const wam_f2 (&fp)[L],
+                                        const float (&rl)[L], const float (&rh)[L], float& a, float& h, float& v,
+                                        float& d) {
+  if constexpr (kPackedTaps<L>) {
+    wam_f2 ah = {0.f, 0.f}, vd = {0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      ah = __builtin_elementwise_fma(fp[k], wam_f2{rl[k], rl[k]}, ah);
+      vd = __builtin_elementwise_fma(fp[k], wam_f2{rh[k], rh[k]}, vd);
+    }
+    a = ah.x;
+    h = ah.y;
+    v = vd.x;
+    d = vd.y;
+  } else {
+    a = h = v = d = 0.f;
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      a = fmaf(flo[k], rl[k], a);
+      h = fmaf(fhi[k], rl[k], h);
+      v = fmaf(flo[k], rh[k], v);
+      d = fmaf(fhi[k], rh[k], d);
+    }
+  }
+}
+
+template <int L>
+__device__ __forceinline__ void hfilter_any(const float* lds, int j, int p, const float (&flo)[L],
+                                            const float (&fhi)[L], const wam_f2 (&fp)[L], float& lo, float& hi) {
+  if constexpr (kPackedTaps<L>) {
+    const wam_f2 r = hfilter_pk<L>(lds, j, p, fp);
+    lo = r.x;
+    hi = r.y;
+  } else {
+    hfilter<L>(lds, j, p, flo, fhi, lo, hi);
+  }
+}
 
 // ------------------------------------------------------------------------------------------------
 template <int L, int CPL, int VEC, int MAXV, bool NOISE>
@@ -59,6 +108,8 @@ __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, 
     flo[k] = filt[k];
     fhi[k] = filt[L + k];
   }
+  wam_f2 fp[L];
+  tap_pairs<L>(flo, fhi, fp);
   // NOISE: planes are (sample, image, channel); the clean input x holds (image, channel)
   int64_t src_plane = plane, img = 0, smp = 0, ch = 0;
   float sg = 0.f;
@@ -101,7 +152,7 @@ __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, 
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int j = min(j0 + lane + 64 * c, mw - 1);  // clamp: the extra lanes compute a duplicate
-      hfilter<L>(lds, j, p, flo, fhi, lo[c], hi[c]);
+      hfilter_any<L>(lds, j, p, flo, fhi, fp, lo[c], hi[c]);
     }
     wsync();
   };
@@ -152,14 +203,8 @@ __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, 
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int j = j0 + lane + 64 * c;
-      float a = 0.f, h = 0.f, v = 0.f, d = 0.f;
-#pragma unroll
-      for (int k = 0; k < L; ++k) {
-        a = fmaf(flo[k], rl[c][k], a);
-        h = fmaf(fhi[k], rl[c][k], h);
-        v = fmaf(flo[k], rh[c][k], v);
-        d = fmaf(fhi[k], rh[c][k], d);
-      }
+      float a, h, v, d;
+      vfilter<L>(flo, fhi, fp, rl[c], rh[c], a, h, v, d);
       if (j < mw && (!kRolledPrologue<L> || i >= i0)) {
         const int64_t o = plane * out_plane + (int64_t)i * mw + j;
         oa[o] = a;
@@ -219,6 +264,8 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
     flo[k] = filt[k];
     fhi[k] = filt[L + k];
   }
+  wam_f2 fp[L];
+  tap_pairs<L>(flo, fhi, fp);
   const float* src = in + img * (C * CIN) * in_plane;
   {
     const PadLane pl = pad_lane(lane, nw, p, WAM_MODE_ZERO);
@@ -267,7 +314,8 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int q = 0; q < CPL; ++q) hfilter<L>(rows[wv][c], jv[q] ? jcol[q] : mw - 1, p, flo, fhi, lo[c][q], hi[c][q]);
+      for (int q = 0; q < CPL; ++q)
+        hfilter_any<L>(rows[wv][c], jv[q] ? jcol[q] : mw - 1, p, flo, fhi, fp, lo[c][q], hi[c][q]);
     wsync();
   };
 
@@ -327,14 +375,8 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
       const int64_t o = (int64_t)i * mw + jcol[q];
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        float a = 0.f, h = 0.f, v = 0.f, d = 0.f;
-#pragma unroll
-        for (int k = 0; k < L; ++k) {
-          a = fmaf(flo[k], rl[c][q][k], a);
-          h = fmaf(fhi[k], rl[c][q][k], h);
-          v = fmaf(flo[k], rh[c][q][k], v);
-          d = fmaf(fhi[k], rh[c][q][k], d);
-        }
+        float a, h, v, d;
+        vfilter<L>(flo, fhi, fp, rl[c][q], rh[c][q], a, h, v, d);
         if (jv[q] && on) {
           const int64_t plane = img * C + c;
           if (!last) ll_out[plane * out_plane + o] = a;

@@ -379,7 +379,9 @@ __global__ void __launch_bounds__(64 * kWavesF) k_mel_fwd(MelGeom g, const float
   const Tabs t = stage_tables<STAGE>(g, N, tables, index, lf, false);
   float2* buf = reinterpret_cast<float2*>(lf + (STAGE ? tab_floats(N, g.n_mels, g.nnz, false) : 0)) + w * (pad(M) + 2);
   const int64_t frames = g.items * g.F, stride = (int64_t)gridDim.x * kWavesF;
-  int64_t q = (int64_t)blockIdx.x * kWavesF + w;
+  // XCD-aware: logically consecutive workgroups (consecutive frames, which share half a frame of
+  // samples) run on one XCD, so the shared half comes from its L2 instead of a second HBM read
+  int64_t q = wam_xcd_block(blockIdx.x, gridDim.x) * kWavesF + w;
   FrameIn<LOGN> in;
   if (q < frames) in.fetch(wave + (q / g.F) * g.T, g.T, (int)(q % g.F), g.hop, g.F, lane);
   for (; q < frames; q += stride) {

@@ -131,6 +131,22 @@ __device__ __forceinline__ void hfilter(const float* lds, int j, int p, const fl
   hi = d;
 }
 
+typedef float wam_f2 __attribute__((ext_vector_type(2)));
+
+// hfilter with (lo, hi) as one packed chain: fp[k] = (flo[k], fhi[k]); the same sums
+template <int L, int PADL = kPadL>
+__device__ __forceinline__ wam_f2 hfilter_pk(const float* lds, int j, int p, const wam_f2 (&fp)[L]) {
+  const float2* s2 = reinterpret_cast<const float2*>(lds + PADL + 2 * j - p);
+  wam_f2 acc = {0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < L; k += 2) {
+    const float2 v = s2[k >> 1];
+    acc = __builtin_elementwise_fma(fp[k], wam_f2{v.x, v.x}, acc);
+    acc = __builtin_elementwise_fma(fp[k + 1], wam_f2{v.y, v.y}, acc);
+  }
+  return acc;
+}
+
 // ------------------------------------------------------------------------------------------------
 // One level's streaming synthesis (waverec2 level) for (strip, coefficient rows [qbeg, qend)) of
 // one wave, shared by the plane-resident synthesis (dwt2_plane.hip) and the per-level kernel
