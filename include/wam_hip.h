@@ -72,8 +72,8 @@ int64_t wam_plan_coeff_numel(const wam_plan* plan);
 /* spatial dims produced by wam_waverec (ptwt: odd n reconstructs to n+1) */
 int wam_plan_rec_shape(const wam_plan* plan, int64_t* dims);
 /* bytes of scratch the transforms need for `batch` items (caller allocates). For 2D plans on the
- * per-level row synthesis it covers the intermediate approximations of 4 IG alphas, which
- * wam_waverec synthesises per level launch (larger workspaces let up to 8 share a launch). */
+ * per-level row synthesis it covers the intermediate approximations of 8 IG alphas, which
+ * wam_waverec synthesises per level launch. */
 int64_t wam_plan_workspace_bytes(const wam_plan* plan, int64_t batch);
 
 /* ------------------------------------------------------------------------------------------------

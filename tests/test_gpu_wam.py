@@ -190,6 +190,6 @@ def test_wam_group_size_invariance(W, monkeypatch):
     x = torch.tensor(rs.standard_normal((3, 3, 224, 224)).astype(np.float32))
     kw = dict(wavelet="db4", J=3, n_samples=7, noise="philox", frame="native", sample_batch=2)
     full = W.WaveletAttribution2D(testmodels.TinySmooth2D().cuda(), **kw)(x, [0, 1, 2])
-    monkeypatch.setattr(m2, "wam_group", lambda model_group, total, per_sample: model_group)
+    monkeypatch.setattr(m2, "wam_group", lambda model_group, total, per_sample, budget=None: model_group)
     small = W.WaveletAttribution2D(testmodels.TinySmooth2D().cuda(), **kw)(x, [0, 1, 2])
     assert np.abs(full - small).max() < 1e-6

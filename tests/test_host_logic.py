@@ -328,3 +328,18 @@ def test_pil_bilinear_tables_reproduce_pillow(hw):
         src = np.stack([np.clip((half + (src[b0:b0 + c] * kv[y, :c, None, None]).sum(0)) >> bits, 0, 255)
                         for y, (b0, c) in enumerate(bv)], 0)
     assert np.array_equal(src.astype(np.uint8), ref)
+
+
+def test_wam_group_budget():
+    """IG / SmoothGrad transform passes: multiples of the model group within the memory budget; the
+    default budget is an eighth of the device's HBM, 8-64 GiB (8 GiB without a GPU)."""
+    from wam_amd.engine import wam_budget_bytes, wam_group
+    b = wam_budget_bytes()
+    assert (8 << 30) <= b <= (64 << 30)
+    if not torch.cuda.is_available():
+        assert b == 8 << 30
+    per = int(1.36e9)
+    assert wam_group(2, 64, per, budget_bytes=8 << 30) == 6
+    assert wam_group(2, 64, per, budget_bytes=36 << 30) == 28
+    assert wam_group(2, 5, per, budget_bytes=36 << 30) == 5
+    assert wam_group(4, 64, 100 << 30, budget_bytes=8 << 30) == 4

@@ -27,7 +27,7 @@ int launch_dwt2_analysis_fused(const wam_plan* p, int64_t batch, const float* in
 // a[i] (scaled by sa[i]) and the shared detail bands (scaled by sd[i]) and writes out[i].
 constexpr int kSynMaxAlpha = 8;
 // alphas whose intermediate LL planes the plan workspace holds at once (2D row-synthesis plans)
-constexpr int kSynWsAlpha = 4;
+constexpr int kSynWsAlpha = 8;
 struct SynBatch {
   const float* a[kSynMaxAlpha];
   float* out[kSynMaxAlpha];

@@ -330,10 +330,24 @@ def chunks(start, stop, size):
     return out
 
 
-def wam_group(model_group, total, bytes_per_sample, budget_bytes=8 << 30):
+def wam_budget_bytes(device=None):
+    """Device memory the WAM buffers of one transform pass may take: an eighth of the device's HBM,
+    8-64 GiB (36 GiB on a 288 GB MI355X). Larger passes read the trapezoid accumulators and the
+    synthesis details fewer times per call."""
+    try:
+        total = torch.cuda.get_device_properties(device).total_memory if torch.cuda.is_available() else 0
+    except (RuntimeError, AssertionError, ValueError):
+        total = 0
+    return int(min(max(total // 8, 8 << 30), 64 << 30))
+
+
+def wam_group(model_group, total, bytes_per_sample, budget_bytes=None):
     """Samples (IG steps) per WAM transform launch: a multiple of the model group, as many as the
-    rank's range and a device-memory budget allow. The transforms then run on thousands of planes
-    per launch (full-chip grids, one launch per pass) while the model still sees `model_group`."""
+    rank's range and a device-memory budget allow (wam_budget_bytes). The transforms then run on
+    thousands of planes per launch (full-chip grids, one launch per pass) while the model still sees
+    `model_group`."""
+    if budget_bytes is None:
+        budget_bytes = wam_budget_bytes()
     k = max(1, int(budget_bytes // max(1, bytes_per_sample)) // max(1, model_group))
     return max(1, min(total, k * model_group))
 

@@ -32,7 +32,7 @@ import torch.nn.functional as F
 
 from . import frames
 from .constants import WaveletDetailTuple2d
-from .engine import (GradModel, LegacyNoise, Shard, auto_group, chunks, ig_weights, model_device,
+from .engine import (GradModel, LegacyNoise, Shard, auto_group, chunks, ig_weights, model_device, wam_budget_bytes,
                      require_gpu_device, wam_group)
 from .plan import (CAP_ADJOINT_MAPS, CAP_NOISY_WAVEDEC, disentangle_scales, frame_accumulate, frame_trapz,
                    get_plan, item_sigma, noise_add, reproject_scales, subband_maps)
@@ -339,7 +339,7 @@ class WaveletAttribution2D(BaseWAM2D):
     # ------------------------------------------------------------------ estimators
     def _wam_group(self, plan, n, c, model_group, total):
         per_sample = 4 * n * (c * plan.coeff_numel + 2 * c * int(np.prod(plan.rec_shape)) + plan.coeff_numel)
-        return wam_group(model_group, total, per_sample)
+        return wam_group(model_group, total, per_sample, wam_budget_bytes(plan.device))
 
     def _gradients(self, imgs, y, groups, n, model_group, batch=None):
         """Input gradients of `groups` stacked reference calls, model run `model_group` at a time;
