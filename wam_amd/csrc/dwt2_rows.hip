@@ -24,6 +24,8 @@
 // Waves are independent (no workgroup barriers). LDS writes and reads of a wave-private row are
 // ordered by the wave's in-order LDS queue; __builtin_amdgcn_wave_barrier() keeps the compiler
 // from reordering them.
+#include <cstdlib>
+
 #include "rowtools.hpp"
 
 namespace {
@@ -521,8 +523,13 @@ template <int L>
 int dispatch_adj(int channels, bool mean_first, int64_t images, const float* in, int nh, int nw, int mh, int mw,
                  const float* filt, float* ll_out, const MapsArgs& ma, hipStream_t st) {
   // up to three output columns per lane: fewer strips (each strip refetches and recommits whole rows)
-  // (three spill the register rings past 12 taps)
-  const int cpl = mw <= 64 ? 1 : (mw <= 128 || L > 12 ? 2 : 3);
+  // WAM_ADJ_LONG_CPL (A/B): columns per lane for filters past 12 taps (default 2)
+  static const int long_cpl = [] {
+    const char* e = getenv("WAM_ADJ_LONG_CPL");
+    const int v = e ? atoi(e) : 2;
+    return v < 1 ? 1 : (v > 3 ? 3 : v);
+  }();
+  const int cpl = mw <= 64 ? 1 : (mw <= 128 ? 2 : (L > 12 ? long_cpl : 3));
   if (channels == 3 && mean_first) {
     if (cpl == 1) return dispatch_adj_c<L, 1, 3, 1>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
     if (cpl == 2) return dispatch_adj_c<L, 1, 3, 2>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
