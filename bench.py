@@ -10,12 +10,14 @@ network). One STEP = one explainer call on the config's whole batch:
   c2  WAM-2D db4 J=3 SmoothGrad n=25, ResNet-50 (bf16, BN folded), batch 64 of 224^2, Philox
       noise, native frame E1 (the reference cannot run db4 SmoothGrad at 224).
       THE metric's config and the default.
-  c3  WAM-1D db6 J=5 SmoothGrad n=25, FtEx audio CNN (bf16 autocast) on the mel front-end,
-      batch 256 clips of 5 s at 16 kHz, Philox noise.
-  c4  WAM-2D sym8 J=5 Integrated Gradients, 64 path steps, ResNet-50 (bf16, BN folded), batch
-      128 of 512^2, native frame E2.
-  c5  WAM-3D haar J=2 SmoothGrad n=25 (symmetric), Voxel3D CNN (bf16 autocast), batch 16 of 128^3,
-      Philox noise, legacy in-loop averaging.
+  c3  WAM-1D db6 J=5 SmoothGrad n=25, FtEx audio CNN (fp32) on the mel front-end, batch 256 clips
+      of 5 s at 16 kHz, Philox noise.
+  c4  WAM-2D sym8 J=5 Integrated Gradients, 64 path steps, ResNet-50 (fp32, BN folded), batch 128
+      of 512^2, native frame E2.
+  c5  WAM-3D haar J=2 SmoothGrad n=25 (symmetric), Voxel3D CNN (fp32), batch 16 of 128^3, Philox
+      noise, legacy in-loop averaging.
+  c3-c5 state no reduced model precision, so their credited value runs the model in fp32 (the
+  reference's); the bf16 model is reported beside it as variants.bf16_model.
 Multi-GPU (one process per GPU, RCCL): the explainer itself shards ONE call of the batch with
 dist=True -- c2/c4 over the batch (each rank a contiguous image range, the per-sample
 batch-global maxima combined by an all-reduce MAX, the rows gathered), c3/c5 over the noise
@@ -39,6 +41,7 @@ The JSON line also carries
 """
 import argparse
 import csv
+import datetime
 import glob
 import json
 import os
@@ -120,7 +123,7 @@ def workload(name):
                         lambda: [int(v) for v in np.random.RandomState(6).randint(0, 50, 256)],
                         lambda: testmodels.FtEx(seed=0),
                         dict(wavelet="db6", J=5, method="smooth", mode="reflect", n_samples=25, sample_rate=16000,
-                             noise="philox"), "bf16",
+                             noise="philox"), "fp32",
                         "c3: WAM-1D db6 J=5 SmoothGrad n_samples=25, batch 256 x 80000 samples, FtEx audio CNN",
                         "samples")
     if name == "c4":
@@ -131,7 +134,7 @@ def workload(name):
                         lambda: [int(v) for v in np.random.RandomState(7).randint(0, 1000, 128)],
                         lambda: testmodels.resnet50(seed=0),
                         dict(wavelet="sym8", J=5, method="integratedgrad", mode="reflect", n_samples=64,
-                             frame="native"), "bf16",
+                             frame="native"), "fp32",
                         "c4: WAM-2D sym8 J=5 Integrated Gradients (64 path steps), batch 128 x 512x512, ResNet-50",
                         "images")
     if name == "c5":
@@ -140,7 +143,7 @@ def workload(name):
                         lambda: [int(v) for v in np.random.RandomState(8).randint(0, 10, 16)],
                         lambda: testmodels.Voxel3D(seed=0),
                         dict(wavelet="haar", J=2, method="smooth", mode="symmetric", n_samples=25,
-                             noise="philox"), "bf16",
+                             noise="philox"), "fp32",
                         "c5: WAM-3D haar J=2 SmoothGrad n_samples=25, batch 16 x 128^3, Voxel3D CNN", "samples")
     raise ValueError(name)
 
@@ -161,6 +164,8 @@ def parse(argv=None):
     ap.add_argument("--pmc", default="auto", choices=["auto", "off"])
     ap.add_argument("--extras", default="auto", choices=["auto", "off"], help="c2 parity / variants / ceilings")
     ap.add_argument("--dist-axis", default=None, choices=["auto", "samples", "images"])
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="seconds a collective may wait before the rank aborts (N > 1)")
     ap.add_argument("--wam-probe", action="store_true", help=argparse.SUPPRESS)  # PMC child run
     # test-only: the process group's backend and every rank on cuda:0 (rehearsing the N > 1 path on
     # a one-GPU box); the driver's runs use the defaults (RCCL, one GPU per rank)
@@ -518,13 +523,14 @@ def cpu_baseline(wl, seconds, x, y):
     t0 = time.perf_counter()
     out = run(n_img, n_s)
     dt = time.perf_counter() - t0
+    per = dt / (n_img * n_s)   # seconds per (item x sample / step) unit
     rec = {"value": n_img * n_s / dt / wl.n_steps, "unit": wl.unit, "cores": cores, "kind": "port",
            "sample": "oracle/wam_ref (reference glue restated on torch-CPU ptwt, numpy legacy noise), fp32 model, "
                      "%d item(s) x %d %s of the %s workload in %.1f s on %d thread(s) of %s%s" % (
                          n_img, n_s, "noise samples" if wl.kw["method"] == "smooth" else "path steps", wl.name, dt,
                          cores, _cpu_model_name(),
                          "" if n_s == wl.n_steps else ", extrapolated to %d per attribution" % wl.n_steps)}
-    return rec, (n_img, n_s, out)
+    return rec, (n_img, n_s, out, per, run)
 
 
 # ============================================================================ c2 extras
@@ -542,7 +548,12 @@ def _top_iou(a, b, frac=0.10):
 
 
 def _cmp(a, b, what):
-    return {"what": what, "rel_l2": round(_rel_l2(a, b), 6), "max_abs": round(float(np.abs(a - b).max()), 6),
+    """a vs the reference b: relative L2, max |a - b| (unrounded) and the same over max |b|, top-10 %
+    IoU of the per-item rankings"""
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    mx = float(np.abs(a - b).max())
+    return {"what": what, "rel_l2": float("%.4g" % _rel_l2(a, b)), "max_abs": float("%.4g" % mx),
+            "max_abs_over_max_ref": float("%.4g" % (mx / max(1e-300, float(np.abs(b).max())))),
             "top10_iou": round(_top_iou(a, b), 4), "items": int(a.shape[0])}
 
 
@@ -551,11 +562,23 @@ def _main_map(o):
     return np.asarray(o[0] if isinstance(o, tuple) else o)
 
 
+# parity blocks cover at least this many items; when the cpu_baseline sample holds fewer, the CPU
+# reference runs again on that many items with fewer noise samples / path steps (same algorithm)
+PARITY_MIN_ITEMS = {"c3": 4, "c4": 4, "c5": 2}
+
+
 def parity_extras(wl, dev, args, ex, x, y, cpu_ref):
     """c3 / c4 / c5: the GPU path (fp32 model as is, the reference's numpy noise for SmoothGrad) vs
     the CPU reference path's own output (cpu_baseline) on the same items, samples / path steps and
     weights; where the headline model runs in bf16, the headline map vs that fp32 map too."""
-    n_img, n_s, ref = cpu_ref
+    n_img, n_s, ref, per, run = cpu_ref
+    want = min(wl.n, PARITY_MIN_ITEMS.get(wl.name, 1))
+    if n_img < want:
+        n_img = want
+        n_s = int(max(2, min(wl.n_steps, args.cpu_seconds * 1.5 / per / want)))
+        log("%s parity: CPU reference on %d items x %d %s" % (wl.name, n_img, n_s,
+                                                              "samples" if wl.kw["method"] == "smooth" else "steps"))
+        ref = run(n_img, n_s)
     yy = y[:n_img] if isinstance(y, list) else y
     smooth = wl.kw.get("method", "smooth") == "smooth"
     ex32 = build_explainer(wl, dev, args, model_dtype="fp32", optimize=False, noise="numpy" if smooth else None)
@@ -567,13 +590,20 @@ def parity_extras(wl, dev, args, ex, x, y, cpu_ref):
                                                  ", numpy noise" if smooth else "",
                                                  "noise" if smooth else "path steps"))}
     par["gpu_fp32_vs_cpu_reference"]["n_samples"] = n_s
-    if (args.model_dtype or wl.model_dtype) == "bf16":
-        hd = build_explainer(wl, dev, args, noise="numpy" if smooth else None)
+    head_dtype = args.model_dtype or wl.model_dtype
+    runs = []
+    if head_dtype == "bf16" or wl.dim == 2:   # c3 / c5 headline at fp32 = the fp32 run above
+        runs.append(("headline_vs_fp32_as_is", {}, "headline model (%s%s)" % (
+            head_dtype, ", BN-folded" if wl.dim == 2 else "")))
+    if head_dtype != "bf16":
+        runs.append(("bf16_variant_vs_fp32_as_is", {"model_dtype": "bf16"}, "bf16 variant model (%s)" % (
+            "BN-folded" if wl.dim == 2 else "autocast")))
+    for tag, kw, what in runs:
+        hd = build_explainer(wl, dev, args, noise="numpy" if smooth else None, **kw)
         hd.n_samples = n_s
-        par["bf16_headline_vs_fp32"] = _cmp(_main_map(hd(x[:n_img], yy)), _main_map(got),
-                                            "headline model (bf16%s) vs fp32 model as is, same items and %s: model "
-                                            "precision only" % (", BN-folded" if wl.dim == 2 else "",
-                                                                "noise" if smooth else "path steps"))
+        par[tag] = _cmp(_main_map(hd(x[:n_img], yy)), _main_map(got),
+                        "%s vs fp32 model as is, same items and %s: model precision / folding only" % (
+                            what, "noise" if smooth else "path steps"))
         del hd
     del ex32
     torch.cuda.empty_cache()
@@ -598,7 +628,7 @@ def c2_extras(wl, dev, args, ex, x, y, cpu_ref):
            "philox_vs_numpy_noise": _cmp(b, c, "fp32 model, Philox vs numpy legacy noise: Monte-Carlo spread of "
                                               "two 25-sample SmoothGrad estimates (context, not an error)")}
     if cpu_ref is not None:
-        n_img, n_s, ref = cpu_ref
+        n_img, n_s, ref = cpu_ref[:3]
         ex_ref = build_explainer(wl, dev, args, model_dtype="fp32", optimize=False, noise="numpy")
         ex_ref.n_samples = n_s
         got = ex_ref(x[:n_img], y[:n_img])
@@ -707,10 +737,14 @@ def main():
         traffic = live_pmc(args.config)  # child processes, BEFORE this process touches the GPU
     if world > 1:
         torch.cuda.set_device(local)
+        # a collective that does not complete within the timeout aborts the rank with the
+        # collective's name (RCCL watchdog) instead of hanging until the driver kills the run
+        tmo = datetime.timedelta(seconds=args.dist_timeout)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "3")
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     import wam_amd  # noqa: F401  (fails loudly without libwam_hip.so)
@@ -791,12 +825,23 @@ def main():
         log("c2 extras: parity, variants, round trip, copy ceiling")
         extras = c2_extras(wl, dev, args, ex, xd, y, cpu_ref)
     elif cpu_ref is not None and wl.name in ("c1",):
-        n_img, n_s, ref = cpu_ref
+        n_img, n_s, ref = cpu_ref[:3]
         extras["parity"] = {"gpu_vs_cpu_reference": _cmp(out[:n_img], ref, "GPU vs CPU reference path, same input, "
                                                                             "weights and numpy noise")}
     elif cpu_ref is not None and args.extras == "auto":
         log("%s extras: parity" % wl.name)
         extras["parity"] = parity_extras(wl, dev, args, ex, xd, y, cpu_ref)
+    if rank == 0 and world == 1 and wl.name in ("c3", "c4", "c5") and args.extras == "auto" and \
+            (args.model_dtype or wl.model_dtype) == "fp32":
+        log("%s variant: bf16 model" % wl.name)
+        e = build_explainer(wl, dev, args, model_dtype="bf16")
+        dtv, _, _ = timed(lambda: e(xd, y), 2, 1, 1, dev)
+        extras["variants"] = {"bf16_model": {
+            "value": round(wl.n * 2 / dtv, 3), "ms_per_step": round(dtv / 2 * 1e3, 2), "steps": 2,
+            "what": "the same call with the model in bf16 (%s): not the credited value, the reference runs fp32"
+                    % ("BN-folded" if wl.dim == 2 else "autocast")}}
+        del e
+        torch.cuda.empty_cache()
 
     model_dtype = args.model_dtype or wl.model_dtype
     total = wl.n * args.steps

@@ -81,10 +81,20 @@ def main():
     for name, dim, model, x, y, kw in cases():
         try:
             cls = getattr(wam_amd, "WaveletAttribution" + dim)
-            ref = flat(cls(model().cuda(), **kw)(x, y))
-            got = flat(cls(model().cuda(), dist=True, **kw)(x, y))
+            m_ref, m_sh = model().cuda(), model().cuda()
+            ref = flat(cls(m_ref, **kw)(x, y))
+            got = flat(cls(m_sh, dist=True, **kw)(x, y))
             err = float(np.abs(got - ref).max() / max(1.0, np.abs(ref).max())) if got.shape == ref.shape else 1e9
-            res[name] = {"err": err, "shape_ok": got.shape == ref.shape}
+            # the model's .grad after the call: per-rank increments summed over the ranks
+            # (engine.param_grad_sum) must equal the single-process call's
+            gerr = 0.0
+            for a, b in zip(m_sh.parameters(), m_ref.parameters()):
+                if (a.grad is None) != (b.grad is None):
+                    gerr = 1e9
+                elif a.grad is not None:
+                    ga, gb = a.grad.double().cpu(), b.grad.double().cpu()
+                    gerr = max(gerr, float((ga - gb).abs().max() / max(1e-30, float(gb.abs().max()))))
+            res[name] = {"err": err, "shape_ok": got.shape == ref.shape, "grad_err": gerr}
         except Exception:
             res[name] = {"error": traceback.format_exc()}
         dist.barrier()

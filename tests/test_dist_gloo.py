@@ -84,6 +84,18 @@ def _worker(rank, world, port, q):
                                          for k in range(len(g) - 1)]
             acc3 += torch.tensor(wam_ref.mosaic_2d(gn, False, (64, 64), (64, 64)))
         res["smooth_images"] = (shard.all_gather_rows(acc3, 3) / 3).numpy()
+        # --- parameter gradients of a sharded call: per-rank increments summed once (every rank
+        # in the same order; rank 1 has no samples of a 1-sample call and contributes zeros)
+        pm = testmodels.TinySmooth2D()
+        xg = torch.tensor(np.random.RandomState(6).standard_normal((3 * 2, 3, 16, 16)).astype(np.float32))
+        for n_smp in (3, 1):
+            for p_ in pm.parameters():
+                p_.grad = None
+            a0, a1 = shard.range(n_smp)
+            with engine.param_grad_sum(engine.trainable_params(pm), shard):
+                if a1 > a0:
+                    engine.input_gradient(pm, xg[2 * a0:2 * a1], [1, 2], a1 - a0, 2)
+            res["pgrad%d" % n_smp] = [p_.grad.clone().numpy() for p_ in pm.parameters()]
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -117,5 +129,12 @@ def test_two_rank_sharding_matches_single_process():
         assert np.array_equal(out[0]["smooth"], out[r]["smooth"])
         ref3 = wam_ref.smooth_2d(testmodels.TinySmooth2D(), torch.tensor(np.random.RandomState(4).standard_normal(
             (3, 3, 64, 64)).astype(np.float32)), [1, 2, 0], wavelet="db2", J=2, n_samples=3, frame="native")
+        for n_smp in (3, 1):
+            pm = testmodels.TinySmooth2D()
+            xg = torch.tensor(np.random.RandomState(6).standard_normal((3 * 2, 3, 16, 16)).astype(np.float32))
+            from wam_amd import engine
+            engine.input_gradient(pm, xg[:2 * n_smp], [1, 2], n_smp, 2)
+            for got, p_ in zip(out[r]["pgrad%d" % n_smp], pm.parameters()):
+                assert np.allclose(got, p_.grad.numpy(), rtol=1e-5, atol=1e-7)
         assert out[r]["smooth_images"].shape == ref3.shape
         assert np.abs(out[r]["smooth_images"] - ref3).max() < 1e-6

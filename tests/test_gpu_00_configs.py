@@ -178,6 +178,81 @@ def test_c4_ig_sym8_j5_512_native(W):
     assert err <= 1e-4 * max(1.0, np.abs(ref).max())
 
 
+def _force_passes(monkeypatch, W, steps_per_pass):
+    """Cap the samples / IG steps per WAM transform pass (engine.wam_group, as the classes call it)
+    so a call runs several passes."""
+    monkeypatch.setattr(W.wam_2D, "wam_group", lambda mg, total, per, budget=None: max(1, min(total, steps_per_pass)))
+
+
+def test_c4_ig_sym8_j5_512_multipass(W, monkeypatch):
+    """The c4 path as the bench times it: IG sym8 J=5 reflect, native frame, 512^2, with the path
+    steps split into several transform passes (25 steps, 10 per pass: passes 10 / 10 / 5) so the
+    trapezoid carries `prev` across passes (k_frame_trapz with k0 > 0) and each pass's synthesis
+    runs its alphas in per-launch groups of 8 with a partial last group (8 + 2, 8 + 2, 5) -- vs
+    oracle.wam_ref.ig_2d (lib/wam_2D.py:437-459); bar 1e-4 * max|ref|."""
+    from oracle import wam_ref
+    _force_passes(monkeypatch, W, 10)
+    rs = np.random.RandomState(41)
+    x = torch.tensor(rs.standard_normal((2, 3, 512, 512)).astype(np.float32))
+    y = [3, 8]
+    n = 25
+    ref = wam_ref.ig_2d(testmodels.TinySmooth2D(), x, y, wavelet="sym8", J=5, mode="reflect", n_samples=n,
+                        frame="native")
+    ex = W.WaveletAttribution2D(testmodels.TinySmooth2D().cuda(), wavelet="sym8", J=5, mode="reflect",
+                                method="integratedgrad", n_samples=n, frame="native", sample_batch=2)
+    out = ex(x, y)
+    assert out.shape == ref.shape == (2, 512, 512)
+    err = np.abs(out - ref).max()
+    print("c4 ig multipass: max abs %.3e (max |ref| %.3e)" % (err, np.abs(ref).max()))
+    assert err <= 1e-4 * max(1.0, np.abs(ref).max())
+    # the same call in one pass agrees to fp32 summation order
+    monkeypatch.undo()
+    one = W.WaveletAttribution2D(testmodels.TinySmooth2D().cuda(), wavelet="sym8", J=5, mode="reflect",
+                                 method="integratedgrad", n_samples=n, frame="native", sample_batch=2)(x, y)
+    assert np.abs(one - out).max() <= 1e-5 * max(1.0, np.abs(ref).max())
+
+
+def test_c2_ig_db4_plane_multipass(W, monkeypatch):
+    """IG on the plane-resident synthesis (db4 J=3 at 224^2, all alphas of a pass in one launch)
+    over several passes (10 steps, 4 per pass) vs oracle.wam_ref.ig_2d."""
+    from oracle import wam_ref
+    _force_passes(monkeypatch, W, 4)
+    rs = np.random.RandomState(42)
+    x = torch.tensor(rs.standard_normal((2, 3, 224, 224)).astype(np.float32))
+    y = [1, 4]
+    ref = wam_ref.ig_2d(testmodels.TinySmooth2D(), x, y, wavelet="db4", J=3, mode="reflect", n_samples=10,
+                        frame="native")
+    out = W.WaveletAttribution2D(testmodels.TinySmooth2D().cuda(), wavelet="db4", J=3, mode="reflect",
+                                 method="integratedgrad", n_samples=10, frame="native", sample_batch=2)(x, y)
+    err = np.abs(out - ref).max()
+    print("c2-geometry ig multipass: max abs %.3e (max |ref| %.3e)" % (err, np.abs(ref).max()))
+    assert err <= 1e-4 * max(1.0, np.abs(ref).max())
+
+
+def test_c2_philox_smooth_multipass(W, monkeypatch):
+    """The c2 perf path (Philox noise fused into k_plane_ana<noise>) over several transform passes
+    (7 samples, 2 per pass: sample_base 0, 2, 4, 6) vs the oracle fed noise_add's values."""
+    from oracle import wam_ref
+    from wam_amd import plan as P
+    _force_passes(monkeypatch, W, 2)
+    rs = np.random.RandomState(43)
+    N, C, H, S = 2, 3, 224, 7
+    x = torch.tensor(rs.standard_normal((N, C, H, H)).astype(np.float32))
+    y = [5, 2]
+    xd = x.cuda()
+    item = C * H * H
+    sigma = P.item_sigma(xd, item, item, 0.25)
+    noise = P.noise_add(torch.zeros_like(xd), sigma, S, N, item, item, seed=42, sample_base=0)
+    noise = noise.view(S, N, C, H, H).cpu().numpy()
+    ref = wam_ref.smooth_2d(testmodels.TinySmooth2D(), x, y, wavelet="db4", J=3, n_samples=S, frame="native",
+                            noise=noise)
+    out = W.WaveletAttribution2D(testmodels.TinySmooth2D().cuda(), wavelet="db4", J=3, n_samples=S,
+                                 noise="philox", frame="native", sample_batch=1)(x, y)
+    err = np.abs(out - ref).max()
+    print("c2 philox multipass: max abs %.3e" % err)
+    assert err < 1e-4
+
+
 def test_alpha_fused_waverec_sym8_512_j5():
     """The per-level sym8 synthesis with the IG alpha fused on the coefficient load equals the
     synthesis of the pre-scaled coefficients fp32(alpha) * c, bit for bit (c4 geometry)."""

@@ -145,6 +145,56 @@ def test_input_gradient_accumulates_parameter_grads_like_reference(y):
     assert all(p.grad is None for p in frozen.parameters())
 
 
+def test_input_gradient_unused_trainable_parameters():
+    """A trainable submodule outside the graph (an eval-mode auxiliary head) gets no gradient and
+    raises nothing, as loss.backward() leaves it (autograd.grad without allow_unused)."""
+    import testmodels
+
+    class WithAux(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.body = testmodels.TinySmooth2D()
+            self.aux = torch.nn.Linear(3, 3)   # never called in forward
+
+        def forward(self, x):
+            return self.body(x)
+
+    torch.manual_seed(2)
+    m = WithAux()
+    img = torch.randn(4, 3, 16, 16)
+    g = engine.input_gradient(m, img, [1, 2], 2, 2)
+    assert g.shape == img.shape and torch.isfinite(g).all()
+    assert m.aux.weight.grad is None and m.aux.bias.grad is None
+    assert all(p.grad is not None for p in m.body.parameters())
+    gm = engine.GradModel(m)
+    assert len(gm.params()) == len(list(m.parameters()))
+    assert engine.GradModel(m, optimize=True).params() == []
+
+
+def test_param_grad_sum_single_rank_is_plain_accumulation():
+    """One rank: param_grad_sum is a no-op and .grad accumulates directly."""
+    import testmodels
+    torch.manual_seed(3)
+    a, b = testmodels.TinySmooth2D(), testmodels.TinySmooth2D()
+    img = torch.randn(2, 3, 16, 16)
+    engine.input_gradient(a, img, 1, 1, 2)
+    with engine.param_grad_sum(engine.trainable_params(b), engine.Shard(None)):
+        engine.input_gradient(b, img, 1, 1, 2)
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.equal(p.grad, q.grad)
+
+
+def test_wam_budget_override():
+    old = engine.BUDGET_BYTES
+    try:
+        engine.BUDGET_BYTES = 12345
+        assert engine.wam_budget_bytes() == 12345
+        assert engine.wam_group(2, 100, 1000, engine.wam_budget_bytes()) == 12
+    finally:
+        engine.BUDGET_BYTES = old
+    assert engine.wam_budget_bytes() >= 1 << 30
+
+
 def test_legacy_noise_stream_matches_reference_loop():
     x = torch.tensor(np.random.RandomState(3).standard_normal((3, 2, 5, 5)).astype(np.float32))
     sig = [float(0.25 * (x[i].max() - x[i].min())) for i in range(3)]

@@ -24,7 +24,6 @@
 // XCD (L2); for noisy analysis the logical order is sample-fastest, so the S noise samples of one
 // clean plane run back to back on one XCD and its rows are read from HBM about once.
 #include <atomic>
-#include <cstdlib>
 
 #include "rowtools.hpp"
 
@@ -762,14 +761,11 @@ PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items
   g.maps_item = p->band_off[p->nbands];
   lds_floats(p, nw0, g.rowlds, g.llcap, noisy);
   g.coop = coop_ok(p, nw0, noisy);
-  // WAM_PLANE_ORDER (A/B): 0 plane-fastest, 1 sample-fastest through the XCD swizzle (default),
-  // 2 sample-fastest as issued (a plane's samples spread over the XCDs)
-  static const int order = [] {
-    const char* e = getenv("WAM_PLANE_ORDER");
-    return e ? atoi(e) : 1;
-  }();
-  g.sample_fast = order != 0;
-  g.xcd_order = order != 2;
+  // noisy analysis: sample-fastest through the XCD swizzle (the S samples of a plane read it from
+  // one L2; plane-fastest and un-swizzled orders measured 684 / 681 vs 666 us,
+  // profiles/r03e_plane_order_ab.log)
+  g.sample_fast = 1;
+  g.xcd_order = 1;
   return g;
 }
 

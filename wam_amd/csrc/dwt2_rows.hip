@@ -24,8 +24,6 @@
 // Waves are independent (no workgroup barriers). LDS writes and reads of a wave-private row are
 // ordered by the wave's in-order LDS queue; __builtin_amdgcn_wave_barrier() keeps the compiler
 // from reordering them.
-#include <cstdlib>
-
 #include "rowtools.hpp"
 
 namespace {
@@ -241,7 +239,19 @@ struct MapsArgs {
 // planes of an image are averaged on the load and ONE plane is filtered (the mean commutes with the
 // linear adjoint -- the k_plane_maps form, equal to fp32 rounding), and the next level's LL is one
 // plane per image. CPL: output columns per lane (strip = 64 CPL columns).
-template <int L, int C, int CIN, int CPL, int VEC, int MAXV>
+// WIN (rows split into strips, 16-byte rows): a wave fetches only its strip's input window --
+// columns [2 j0 - PW, 2 j0 - PW + WN) with PW = p rounded up to 4 -- instead of the whole row:
+// every strip fetching whole rows read each row nstrips times from L2, and at c4's 28 alphas per
+// launch enough of those re-reads missed L2 to make the level-0 kernel move 1.62x its bytes from
+// HBM (profiles/r03l_bench_c4.log). Zero mode: window columns outside the row load as zeros.
+template <int L, int CPL>
+struct AdjWindow {
+  static constexpr int PW = (L - 2 + 3) & ~3;
+  static constexpr int WN = PW + 128 * CPL + 4;         // floats, multiple of 4
+  static constexpr int MAXV = (WN + 255) / 256;         // float4 loads per lane
+};
+
+template <int L, int C, int CIN, int CPL, int VEC, int MAXV, bool WIN = false>
 __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, int nh, int nw, int64_t in_plane,
                                                   float* __restrict__ ll_out, int mh, int mw,
                                                   const float* __restrict__ filt, int nstrips, int nchunks, int R,
@@ -290,12 +300,38 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
   const int64_t out_plane = (int64_t)mh * mw;
 
   constexpr int NF = C * CIN;  // source rows fetched per extended row
+  static_assert(!WIN || VEC == 4, "windowed rows are fetched as float4");
+  constexpr int PW = AdjWindow<L, CPL>::PW;
+  // window mode: the row buffer holds columns ws .. ws + WN - 1 (ws a multiple of 4); a global
+  // output column j reads LDS column 2 (j - j0) + PW - p, i.e. hfilter with (j - j0, p - PW)
+  const int j0w = strip * 64 * CPL;
+  const int ws = 2 * j0w - PW;
+  const int jofs = WIN ? j0w : 0;
+  const int peff = WIN ? p - PW : p;
   RowRegs<VEC, MAXV> f[2][NF];
   auto fetch = [&](RowRegs<VEC, MAXV> (&r)[NF], int er) {
     const bool valid = er >= 0 && er < nh;  // zero padding
     const int rr = valid ? er : 0;
+    if constexpr (WIN) {
 #pragma unroll
-    for (int c = 0; c < NF; ++c) r[c].fetch(src + c * in_plane + (int64_t)rr * nw, nw, lane, valid);
+      for (int c = 0; c < NF; ++c) {
+        const float* row = src + c * in_plane + (int64_t)rr * nw;
+#pragma unroll
+        for (int q = 0; q < MAXV; ++q) {
+          const int col = ws + (lane + 64 * q) * 4;
+          r[c].ok[q] = valid && col >= 0 && col < nw;  // whole float4s: ws and nw are multiples of 4
+          const int ci = min(max(col, 0), nw - 4);
+          const float4 t = *reinterpret_cast<const float4*>(row + ci);
+          r[c].v[4 * q] = t.x;
+          r[c].v[4 * q + 1] = t.y;
+          r[c].v[4 * q + 2] = t.z;
+          r[c].v[4 * q + 3] = t.w;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < NF; ++c) r[c].fetch(src + c * in_plane + (int64_t)rr * nw, nw, lane, valid);
+    }
   };
   auto process = [&](RowRegs<VEC, MAXV> (&r)[NF], float (&lo)[C][CPL], float (&hi)[C][CPL]) {
     if constexpr (CIN > 1) {  // ((g0 + g1) + g2) * (1 / CIN), as k_plane_maps averages on its load
@@ -317,7 +353,7 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int q = 0; q < CPL; ++q)
-        hfilter_any<L>(rows[wv][c], jv[q] ? jcol[q] : mw - 1, p, flo, fhi, fp, lo[c][q], hi[c][q]);
+        hfilter_any<L>(rows[wv][c], (jv[q] ? jcol[q] : mw - 1) - jofs, peff, flo, fhi, fp, lo[c][q], hi[c][q]);
     wsync();
   };
 
@@ -489,7 +525,7 @@ int dispatch_ana(int64_t batch, const float* in, int nh, int nw, int mh, int mw,
   return dispatch_ana_cpl<L, 1>(batch, in, nh, nw, mh, mw, mode, filt, oa, oh, ov, od, nz, st);
 }
 
-template <int L, int C, int CIN, int CPL, int VEC, int MAXV>
+template <int L, int C, int CIN, int CPL, int VEC, int MAXV, bool WIN = false>
 int launch_adj_t(int64_t images, const float* in, int nh, int nw, int mh, int mw, const float* filt, float* ll_out,
                  const MapsArgs& ma, hipStream_t st) {
   const int nstrips = (mw + 64 * CPL - 1) / (64 * CPL);
@@ -500,7 +536,7 @@ int launch_adj_t(int64_t images, const float* in, int nh, int nw, int mh, int mw
   double bytes = 4.0 * (double)images * ((double)C * CIN * nh * nw + 4.0 * mh * mw + (last ? 0.0 : (double)C * mh * mw) +
                                          (ma.full ? (double)C * 4 * mh * mw : 0.0));
   WamTimer tm(st, "k_adj_maps", bytes);
-  hipLaunchKernelGGL((k_adj_maps<L, C, CIN, CPL, VEC, MAXV>), dim3((unsigned)((waves + kWaves - 1) / kWaves)),
+  hipLaunchKernelGGL((k_adj_maps<L, C, CIN, CPL, VEC, MAXV, WIN>), dim3((unsigned)((waves + kWaves - 1) / kWaves)),
                      dim3(256), 0, st, in, nh, nw, (int64_t)nh * nw, ll_out, mh, mw, filt, nstrips, nchunks, R, waves,
                      ma);
   WAM_LAUNCH_CHECK();
@@ -511,6 +547,10 @@ template <int L, int C, int CIN, int CPL>
 int dispatch_adj_c(int64_t images, const float* in, int nh, int nw, int mh, int mw, const float* filt, float* ll_out,
                    const MapsArgs& ma, hipStream_t st) {
   const bool vec4 = (nw % 4 == 0) && ((uintptr_t)in % 16 == 0);
+  // several strips per row: each wave fetches its strip's window only (AdjWindow)
+  constexpr int WMAXV = AdjWindow<L, CPL>::MAXV;
+  if (vec4 && nw > 256 && mw > 64 * CPL && WMAXV <= 2)
+    return launch_adj_t<L, C, CIN, CPL, 4, WMAXV, true>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
   if (vec4)
     return nw <= 256 ? launch_adj_t<L, C, CIN, CPL, 4, 1>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st)
                      : launch_adj_t<L, C, CIN, CPL, 4, 2>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
@@ -522,14 +562,9 @@ int dispatch_adj_c(int64_t images, const float* in, int nh, int nw, int mh, int 
 template <int L>
 int dispatch_adj(int channels, bool mean_first, int64_t images, const float* in, int nh, int nw, int mh, int mw,
                  const float* filt, float* ll_out, const MapsArgs& ma, hipStream_t st) {
-  // up to three output columns per lane: fewer strips (each strip refetches and recommits whole rows)
-  // WAM_ADJ_LONG_CPL (A/B): columns per lane for filters past 12 taps (default 2)
-  static const int long_cpl = [] {
-    const char* e = getenv("WAM_ADJ_LONG_CPL");
-    const int v = e ? atoi(e) : 2;
-    return v < 1 ? 1 : (v > 3 ? 3 : v);
-  }();
-  const int cpl = mw <= 64 ? 1 : (mw <= 128 ? 2 : (L > 12 ? long_cpl : 3));
+  // up to three output columns per lane: fewer strips; filters past 12 taps keep two (their
+  // (lo, hi) rings of 2 x L registers per column)
+  const int cpl = mw <= 64 ? 1 : (mw <= 128 ? 2 : (L > 12 ? 2 : 3));
   if (channels == 3 && mean_first) {
     if (cpl == 1) return dispatch_adj_c<L, 1, 3, 1>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);
     if (cpl == 2) return dispatch_adj_c<L, 1, 3, 2>(images, in, nh, nw, mh, mw, filt, ll_out, ma, st);

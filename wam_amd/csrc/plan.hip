@@ -199,18 +199,25 @@ static bool syn_rows_alpha_batched(const wam_plan* p) {
          ((p->flags & (WAM_PLAN_NO_ROWS | WAM_PLAN_NO_PLANE)) || !dwt2_plane_syn_supported(p));
 }
 
+// floats per synthesis LL slot (the largest intermediate approximation of the batch), rounded up
+// to 4 floats: slots stay 16-byte aligned, so the float2 output stores of the row synthesis
+// (rowtools.hpp syn_stream, vec2 on even level widths) land on 8-byte aligned addresses whatever
+// the batch and level sizes (an odd count, e.g. db3 at 226^2 with an odd batch, misaligned them)
+static int64_t syn_ll_stride(const wam_plan* p, int64_t batch) {
+  int64_t rec_ll = 0;
+  for (int l = p->levels - 1; l >= 1; --l) {
+    const int64_t v = batch * wam_prod(p->lout[l - 1], p->ndim);
+    if (v > rec_ll) rec_ll = v;
+  }
+  return (rec_ll + 3) & ~(int64_t)3;
+}
+
 extern "C" int64_t wam_plan_workspace_bytes(const wam_plan* p, int64_t batch) {
   if (!p || batch < 0) return -1;
   int nd = p->ndim;
   // LL ping-pong for analysis / adjoint (level 0 output) and A ping-pong for synthesis
   int64_t ll = batch * wam_prod(p->lout[0], nd);
-  int64_t rec_ll = 0;
-  for (int l = p->levels - 1; l >= 1; --l) {
-    int64_t d[WAM_MAX_NDIM];
-    for (int a = 0; a < nd; ++a) d[a] = p->lout[l - 1][a];
-    int64_t v = batch * wam_prod(d, nd);
-    if (v > rec_ll) rec_ll = v;
-  }
+  const int64_t rec_ll = syn_ll_stride(p, batch);
   int64_t tmp_a = 0;
   int64_t rec0[WAM_MAX_NDIM];
   for (int a = 0; a < nd; ++a) rec0[a] = p->rec_shape[a];
@@ -507,11 +514,7 @@ int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const flo
   }
   int nd = p->ndim;
   int64_t out_item = wam_prod(p->rec_shape, nd);
-  int64_t rec_ll = 0;
-  for (int l = p->levels - 1; l >= 1; --l) {
-    int64_t v = batch * wam_prod(p->lout[l - 1], nd);
-    if (v > rec_ll) rec_ll = v;
-  }
+  const int64_t rec_ll = syn_ll_stride(p, batch);
   float* w = (float*)ws;
   if (nd == 2 && !(p->flags & WAM_PLAN_GENERIC) && dwt2_fused_supported(p)) {
     // alphas in groups: one launch per level per group, each level's detail bands read once per

@@ -13,7 +13,9 @@ lib/wam_3D.py:237-238). The same backward here takes ``torch.autograd.grad`` wit
 input and to those parameters and adds the latter into ``.grad`` -- the sum over the stacked
 groups is the sum of the reference's per-call gradients. A model whose parameters are frozen
 (requires_grad False, as the bench does) pays for the input gradient only. ``optimize_model=True``
-runs a folded copy of the model and does not touch the user's parameters.
+runs a folded copy of the model and does not touch the user's parameters. Sharded calls
+(dist=True) all-reduce the increments once per call (``param_grad_sum``), so every rank's .grad
+holds the single-process gradient.
 """
 import collections
 import contextlib
@@ -89,23 +91,71 @@ def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=
     with torch.enable_grad():
         with ctx:
             out = model(inp)
+        # allow_unused: parameters outside the graph (an eval-mode auxiliary head, a conditional
+        # branch) get no gradient, exactly as loss.backward() leaves their .grad untouched
         if y_none_mean:
             scale = None
-            gs = torch.autograd.grad(out.float().mean(), [img] + params)
+            gs = torch.autograd.grad(out.float().mean(), [img] + params, allow_unused=True)
         else:
             seed, scale = seed_gradient(out, y, groups, n, unit=out.dtype != torch.float32, batch=batch)
-            gs = torch.autograd.grad(out, [img] + params, grad_outputs=seed)
+            gs = torch.autograd.grad(out, [img] + params, grad_outputs=seed, allow_unused=True)
     g = gs[0]
+    if g is None:
+        raise RuntimeError("the model's output does not depend on its input")
     if scale is not None:
         g = g * scale
     with torch.no_grad():
         for p, gp in zip(params, gs[1:]):
+            if gp is None:
+                continue
             gp = gp if scale is None else gp * scale
-            if p.grad is None:
-                p.grad = gp.to(p.dtype).clone()
-            else:
-                p.grad.add_(gp.to(p.grad.dtype))
+            _accumulate_param_grad(p, gp)
     return g.contiguous()
+
+
+# Parameter gradients of a sharded call (dist=True): while a `param_grad_sum` block is open the
+# per-rank increments are collected here instead of in .grad, then summed over the ranks once and
+# added to .grad -- every rank ends with the single-process call's gradient, as the reference's
+# loss.backward() leaves it (lib/wam_2D.py:116).
+_PARAM_SINK = None
+
+
+def _accumulate_param_grad(p, gp):
+    if _PARAM_SINK is not None:
+        prev = _PARAM_SINK.get(p)
+        _PARAM_SINK[p] = gp.float().clone() if prev is None else prev.add_(gp.float())
+        return
+    if p.grad is None:
+        p.grad = gp.to(p.dtype).clone()
+    else:
+        p.grad.add_(gp.to(p.grad.dtype))
+
+
+@contextlib.contextmanager
+def param_grad_sum(params, shard):
+    """Collect the parameter-gradient increments of one sharded call and all-reduce them (SUM,
+    one flat buffer, every rank in the same parameter order -- a rank with no work contributes
+    zeros) before adding them to .grad. A no-op for one rank or a model without trainable
+    parameters."""
+    global _PARAM_SINK
+    params = list(params)
+    if shard.world == 1 or not params:
+        yield
+        return
+    prev, _PARAM_SINK = _PARAM_SINK, {}
+    try:
+        yield
+        sink = _PARAM_SINK
+    finally:
+        _PARAM_SINK = prev
+    flat = torch.cat([(sink[p] if p in sink else torch.zeros(p.shape, dtype=torch.float32, device=p.device))
+                      .reshape(-1) for p in params])
+    shard.all_reduce_sum(flat)
+    off = 0
+    for p in params:
+        gp = flat[off:off + p.numel()].view(p.shape)
+        off += p.numel()
+        _accumulate_param_grad(p, gp)
 
 
 class GradModel:
@@ -131,6 +181,10 @@ class GradModel:
             else:
                 self._run = self.model
         return self._run
+
+    def params(self):
+        """The parameters whose .grad a call accumulates (none for the folded copy)."""
+        return [] if self.optimize else trainable_params(self.model)
 
     def __call__(self, img, y, groups, n, y_none_mean=False, batch=None):
         run = self._runner()
@@ -284,6 +338,15 @@ class Shard:
             tdist.all_reduce(t, op=tdist.ReduceOp.MAX, group=self.group)
         return t
 
+    def agree_min(self, value, device):
+        """The smallest of the ranks' `value`s (an int), on every rank: sizes that decide how many
+        collectives a rank issues must be the same everywhere."""
+        if self.world == 1:
+            return int(value)
+        t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MIN, group=self.group)
+        return int(t.item())
+
     def all_gather_rows(self, t, n):
         """t: this rank's rows [range(n)] of an [n, ...] tensor -> the whole tensor on every rank
         (ragged ranges padded to the longest for the collective)."""
@@ -330,15 +393,32 @@ def chunks(start, stop, size):
     return out
 
 
+BUDGET_BYTES = None   # explicit override of wam_budget_bytes (bytes), e.g. for memory-tight models
+
+
 def wam_budget_bytes(device=None):
     """Device memory the WAM buffers of one transform pass may take: an eighth of the device's HBM,
-    8-64 GiB (36 GiB on a 288 GB MI355X). Larger passes read the trapezoid accumulators and the
-    synthesis details fewer times per call."""
+    8-64 GiB (36 GiB on a 288 GB MI355X), capped by half of what is free on the device now (free
+    HBM plus this process's cached, unallocated blocks: the model's own footprint and other
+    processes are already out of it) and shared by the ranks of this node that use the same device.
+    Larger passes read the trapezoid accumulators and the synthesis details fewer times per call.
+    BUDGET_BYTES overrides it."""
+    if BUDGET_BYTES is not None:
+        return int(BUDGET_BYTES)
+    budget = 8 << 30
     try:
-        total = torch.cuda.get_device_properties(device).total_memory if torch.cuda.is_available() else 0
+        if torch.cuda.is_available():
+            total = torch.cuda.get_device_properties(device).total_memory
+            budget = min(max(total // 8, 8 << 30), 64 << 30)
+            free, _ = torch.cuda.mem_get_info(device)
+            free += torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
+            import os
+            local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+            share = max(1, -(-local // max(1, torch.cuda.device_count())))
+            budget = min(budget, max(free // 2, 1 << 30) // share)
     except (RuntimeError, AssertionError, ValueError):
-        total = 0
-    return int(min(max(total // 8, 8 << 30), 64 << 30))
+        pass
+    return int(budget)
 
 
 def wam_group(model_group, total, bytes_per_sample, budget_bytes=None):

@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, LegacyNoise, model_device,
-                     require_gpu_device)
+                     param_grad_sum, require_gpu_device, trainable_params)
 from .melspec import kernel_supported, mel_adjoint, mel_forward, melspec_db
 from .plan import CAP_NOISY_WAVEDEC, accumulate_f32, get_plan, item_sigma, noise_add, trapz_stream
 
@@ -209,23 +209,24 @@ class WaveletAttribution1D(BaseWAM1D):
         self._mel_shape = (n, 1, plan.rec_shape[0] // (self.n_fft // 2) + 1, self.n_mels)
         mel_acc = torch.zeros(int(np.prod(self._mel_shape)), dtype=torch.float32, device=dev)
         c_acc = torch.zeros(n * plan.coeff_numel, dtype=torch.float32, device=dev)
-        for s0, cnt in chunks(s_lo, s_hi, group):
-            if legacy is None and plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
-                flat = plan.wavedec_noisy(x, sigma, cnt, n, 1, self.random_seed, s0)
-            else:
-                host = None if legacy is None else legacy.chunk(s0, cnt)
-                noisy = noise_add(x, sigma, cnt, n, w, w, seed=self.random_seed, sample_base=s0, host_noise=host)
-                flat = plan.wavedec(noisy.view(cnt * n, w))
-            g_mel, cg = self._grads(plan, flat, cnt * n, y, cnt, n)
-            if g_mel.numel() != cnt * mel_acc.numel():
-                raise RuntimeError("melspec gradient shape %s does not match %s" % (tuple(g_mel.shape),
-                                                                                     self._mel_shape))
-            accumulate_f32(g_mel, cnt, mel_acc)
-            for b in range(plan.nbands):
-                nb = int(np.prod(plan.band_shapes[b]))
-                src = cg[cnt * n * plan.band_offsets[b]:cnt * n * (plan.band_offsets[b] + nb)]
-                accumulate_f32(src, cnt, c_acc[n * plan.band_offsets[b]:n * (plan.band_offsets[b] + nb)])
-            self.wam._record(plan, flat, cnt * n, (cnt - 1) * n, cg, cnt * n, (cnt - 1) * n, n)
+        with param_grad_sum(trainable_params(self.model), shard):
+            for s0, cnt in chunks(s_lo, s_hi, group):
+                if legacy is None and plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
+                    flat = plan.wavedec_noisy(x, sigma, cnt, n, 1, self.random_seed, s0)
+                else:
+                    host = None if legacy is None else legacy.chunk(s0, cnt)
+                    noisy = noise_add(x, sigma, cnt, n, w, w, seed=self.random_seed, sample_base=s0, host_noise=host)
+                    flat = plan.wavedec(noisy.view(cnt * n, w))
+                g_mel, cg = self._grads(plan, flat, cnt * n, y, cnt, n)
+                if g_mel.numel() != cnt * mel_acc.numel():
+                    raise RuntimeError("melspec gradient shape %s does not match %s" % (tuple(g_mel.shape),
+                                                                                         self._mel_shape))
+                accumulate_f32(g_mel, cnt, mel_acc)
+                for b in range(plan.nbands):
+                    nb = int(np.prod(plan.band_shapes[b]))
+                    src = cg[cnt * n * plan.band_offsets[b]:cnt * n * (plan.band_offsets[b] + nb)]
+                    accumulate_f32(src, cnt, c_acc[n * plan.band_offsets[b]:n * (plan.band_offsets[b] + nb)])
+                self.wam._record(plan, flat, cnt * n, (cnt - 1) * n, cg, cnt * n, (cnt - 1) * n, n)
         if legacy is not None:
             legacy.finish()
         shard.all_reduce_sum(mel_acc)
@@ -260,18 +261,19 @@ class WaveletAttribution1D(BaseWAM1D):
         mel_prev = torch.zeros_like(mel_acc)
         c_acc = torch.zeros(n * plan.coeff_numel, dtype=torch.float32, device=dev)
         c_prev = torch.zeros_like(c_acc)
-        for k0, cnt in chunks(k_lo, k_hi, group):
-            img = plan.waverec(z, n, alphas=alphas[k0:k0 + cnt]).view(cnt * n, -1)
-            g_mel, cg = self._grads_from_rec(plan, img, y, cnt, n)
-            weights = None
-            if shard.world > 1:
-                weights = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
-            trapz_stream(g_mel, cnt, k0, mel_prev, mel_acc, weights)
-            for b in range(plan.nbands):
-                nb = int(np.prod(plan.band_shapes[b]))
-                lo, hi = n * plan.band_offsets[b], n * (plan.band_offsets[b] + nb)
-                src = cg[cnt * n * plan.band_offsets[b]:cnt * n * (plan.band_offsets[b] + nb)]
-                trapz_stream(src, cnt, k0, c_prev[lo:hi], c_acc[lo:hi], weights)
+        with param_grad_sum(trainable_params(self.model), shard):
+            for k0, cnt in chunks(k_lo, k_hi, group):
+                img = plan.waverec(z, n, alphas=alphas[k0:k0 + cnt]).view(cnt * n, -1)
+                g_mel, cg = self._grads_from_rec(plan, img, y, cnt, n)
+                weights = None
+                if shard.world > 1:
+                    weights = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
+                trapz_stream(g_mel, cnt, k0, mel_prev, mel_acc, weights)
+                for b in range(plan.nbands):
+                    nb = int(np.prod(plan.band_shapes[b]))
+                    lo, hi = n * plan.band_offsets[b], n * (plan.band_offsets[b] + nb)
+                    src = cg[cnt * n * plan.band_offsets[b]:cnt * n * (plan.band_offsets[b] + nb)]
+                    trapz_stream(src, cnt, k0, c_prev[lo:hi], c_acc[lo:hi], weights)
         shard.all_reduce_sum(mel_acc)
         shard.all_reduce_sum(c_acc)
         mel = base_mel.cpu().numpy() * mel_acc.view(base_mel.shape).cpu().numpy()

@@ -32,8 +32,8 @@ import torch.nn.functional as F
 
 from . import frames
 from .constants import WaveletDetailTuple2d
-from .engine import (GradModel, LegacyNoise, Shard, auto_group, chunks, ig_weights, model_device, wam_budget_bytes,
-                     require_gpu_device, wam_group)
+from .engine import (GradModel, LegacyNoise, Shard, auto_group, chunks, ig_weights, model_device, param_grad_sum,
+                     require_gpu_device, wam_budget_bytes, wam_group)
 from .plan import (CAP_ADJOINT_MAPS, CAP_NOISY_WAVEDEC, disentangle_scales, frame_accumulate, frame_trapz,
                    get_plan, item_sigma, noise_add, reproject_scales, subband_maps)
 
@@ -337,9 +337,15 @@ class WaveletAttribution2D(BaseWAM2D):
             self._scales_res = reproject_scales(avg_dev.contiguous(), self.J, self.approx_coeffs)
 
     # ------------------------------------------------------------------ estimators
-    def _wam_group(self, plan, n, c, model_group, total):
+    def _wam_group(self, plan, n, c, model_group, total, shard, axis):
+        """Samples / IG steps per transform pass. On the images axis every rank cuts the range at
+        the same points (one all-reduce MAX of the band maxima per pass), so the memory budget,
+        which follows each device's free memory, is agreed on first (MIN over the ranks)."""
         per_sample = 4 * n * (c * plan.coeff_numel + 2 * c * int(np.prod(plan.rec_shape)) + plan.coeff_numel)
-        return wam_group(model_group, total, per_sample, wam_budget_bytes(plan.device))
+        budget = wam_budget_bytes(plan.device)
+        if axis == "images":
+            budget = shard.agree_min(budget, plan.device)
+        return wam_group(model_group, total, per_sample, budget)
 
     def _gradients(self, imgs, y, groups, n, model_group, batch=None):
         """Input gradients of `groups` stacked reference calls, model run `model_group` at a time;
@@ -392,30 +398,31 @@ class WaveletAttribution2D(BaseWAM2D):
         n_ref = self._group_items(shard, axis, N, n)
         group = auto_group(self.model, n_ref, self.sample_batch)
         # parity mode streams the host-generated legacy noise one model group at a time
-        wgroup = group if self.noise == "numpy" else self._wam_group(plan, n_ref, c, group, s_hi - s_lo)
+        wgroup = group if self.noise == "numpy" else self._wam_group(plan, n_ref, c, group, s_hi - s_lo, shard, axis)
         frame = torch.zeros(n * rh * rw, dtype=torch.float64, device=dev)
         legacy = None
         if self.noise == "numpy":
             legacy = LegacyNoise(sigma_all.cpu().numpy(), (c, h, w), self.random_seed, self.n_samples, dev)
         rec = plan.rec_shape
         last = None
-        for s0, cnt in chunks(s_lo, s_hi, wgroup):
-            if legacy is not None:
-                noisy = noise_add(xs, sigma, cnt, n, item, item, host_noise=legacy.chunk(s0, cnt, i_lo, i_hi))
-                flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
-            elif plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
-                flat = plan.wavedec_noisy(xs, sigma, cnt, n, c, self.random_seed, s0, image_base=i_lo)
-            else:
-                noisy = noise_add(xs, sigma, cnt, n, item, item, seed=self.random_seed, sample_base=s0, item_base=i_lo)
-                flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
-            img = plan.waverec(flat, cnt * n * c)[0].view((cnt * n, c) + rec)
-            g = self._gradients(img, y, cnt, n, group, batch)
-            maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
-            if axis == "images":
-                shard.all_reduce_max(bmax)  # per-sample maxima over the whole batch (A.6)
-            frame_accumulate(cnt, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, frame)
-            last = (plan, flat, None, cnt * n * c, (cnt - 1) * n, n, c)
-            last_g = g[(cnt - 1) * n:].reshape((n * c,) + rec)
+        with param_grad_sum(self._grad.params(), shard):  # .grad as one process leaves it
+            for s0, cnt in chunks(s_lo, s_hi, wgroup):
+                if legacy is not None:
+                    noisy = noise_add(xs, sigma, cnt, n, item, item, host_noise=legacy.chunk(s0, cnt, i_lo, i_hi))
+                    flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
+                elif plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
+                    flat = plan.wavedec_noisy(xs, sigma, cnt, n, c, self.random_seed, s0, image_base=i_lo)
+                else:
+                    noisy = noise_add(xs, sigma, cnt, n, item, item, seed=self.random_seed, sample_base=s0, item_base=i_lo)
+                    flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
+                img = plan.waverec(flat, cnt * n * c)[0].view((cnt * n, c) + rec)
+                g = self._gradients(img, y, cnt, n, group, batch)
+                maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
+                if axis == "images":
+                    shard.all_reduce_max(bmax)  # per-sample maxima over the whole batch (A.6)
+                frame_accumulate(cnt, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, frame)
+                last = (plan, flat, None, cnt * n * c, (cnt - 1) * n, n, c)
+                last_g = g[(cnt - 1) * n:].reshape((n * c,) + rec)
         if legacy is not None:
             legacy.finish()
         if last is not None:
@@ -447,24 +454,25 @@ class WaveletAttribution2D(BaseWAM2D):
         alphas = np.linspace(0, 1, self.n_samples)
         n_ref = self._group_items(shard, axis, N, n)
         group = auto_group(self.model, n_ref, self.sample_batch)
-        wgroup = self._wam_group(plan, n_ref, c, group, k_hi - k_lo)
+        wgroup = self._wam_group(plan, n_ref, c, group, k_hi - k_lo, shard, axis)
         acc = torch.zeros(n * rh * rw, dtype=torch.float32, device=dev)
         prev = torch.zeros_like(acc)
         rec = plan.rec_shape
         last = None
-        for k0, cnt in chunks(k_lo, k_hi, wgroup):
-            img = plan.waverec(z, n * c, alphas=alphas[k0:k0 + cnt]).view((cnt * n, c) + rec)
-            g = self._gradients(img, y, cnt, n, group, batch)
-            maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
-            if axis == "images":
-                shard.all_reduce_max(bmax)
-            weights = None
-            if axis == "samples" and shard.world > 1:
-                weights = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
-            frame_trapz(cnt, k0, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, prev, acc,
-                        weights)
-            last = (plan, float(alphas[k0 + cnt - 1]))
-            last_g = g[(cnt - 1) * n:].reshape((n * c,) + rec)
+        with param_grad_sum(self._grad.params(), shard):
+            for k0, cnt in chunks(k_lo, k_hi, wgroup):
+                img = plan.waverec(z, n * c, alphas=alphas[k0:k0 + cnt]).view((cnt * n, c) + rec)
+                g = self._gradients(img, y, cnt, n, group, batch)
+                maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
+                if axis == "images":
+                    shard.all_reduce_max(bmax)
+                weights = None
+                if axis == "samples" and shard.world > 1:
+                    weights = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
+                frame_trapz(cnt, k0, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, prev, acc,
+                            weights)
+                last = (plan, float(alphas[k0 + cnt - 1]))
+                last_g = g[(cnt - 1) * n:].reshape((n * c,) + rec)
         if last is not None:
             plan_, alpha = last
             coeff = z * float(np.float32(alpha))  # the path coefficients alpha * z of the last step

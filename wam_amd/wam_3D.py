@@ -20,7 +20,7 @@ import torch
 from . import frames
 from .constants import KEYS3
 from .engine import (LegacyNoise, Shard, auto_group, chunks, ig_weights, input_gradient, legacy3d_weights,
-                     model_device, require_gpu_device)
+                     model_device, param_grad_sum, require_gpu_device, trainable_params)
 from ._lib import check, lib, ptr, stream_of
 from .plan import CAP_NOISY_WAVEDEC, cube_accumulate, get_plan, item_sigma, noise_add, subband_maps
 
@@ -58,14 +58,7 @@ class BaseWAM3D:
     @property
     def coeffs(self):
         if self._coeffs is None and self._coeffs_src is not None:
-            plan, flat, items, first, n, c = self._coeffs_src
-            views = [v[first * c:(first + n) * c].detach().cpu().numpy() for v in plan.split(flat, items)]
-            out = []
-            for k in range(n):
-                sq = [views[b][k * c:(k + 1) * c].squeeze() for b in range(plan.nbands)]
-                out.append([sq[0]] + [{key: sq[1 + 7 * lv + j] for j, key in enumerate(KEYS3)}
-                                      for lv in range(plan.levels)])
-            self._coeffs = out
+            self._coeffs = self._item_lists(*self._coeffs_src)
         return self._coeffs
 
     @coeffs.setter
@@ -290,28 +283,29 @@ class WaveletAttribution3D(BaseWAM3D):
             legacy = LegacyNoise(sigma.cpu().numpy(), sp, self.random_seed, self.n_samples, dev)
         acc = torch.zeros(n * S ** 3, dtype=torch.float32, device=dev)
         ns = self.n_samples
-        for s0, cnt in chunks(s_lo, s_hi, group):
-            host = None
-            if legacy is not None:
-                host = legacy.chunk(s0, cnt)  # [cnt, n, *sp]
-                if c > 1:  # the reference noises channel 0 only
-                    full = torch.zeros((cnt, n, c) + sp, dtype=torch.float32, device=dev)
-                    full[:, :, 0] = host
-                    host = full
-            if host is None and c == 1 and plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
-                flat = plan.wavedec_noisy(x, sigma, cnt, n, 1, self.random_seed, s0)
-            else:
-                noisy = noise_add(x, sigma, cnt, n, c * vol, vol, seed=self.random_seed, sample_base=s0,
-                                  host_noise=host)
-                flat = plan.wavedec(noisy.view((cnt * n * c,) + sp))
-            cg = self._grads(plan, flat, cnt * n * c, y, cnt, n, c)
-            if shard.world == 1:
-                self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 0, n_total=float(ns))
-            else:
-                w = torch.from_numpy(legacy3d_weights(s0, cnt, ns)).to(dev)
-                self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 1, weights=w)
-            self.wam._coeffs_src = (plan, flat, cnt * n * c, (cnt - 1) * n, n, c)
-            self.wam._coeffs = None
+        with param_grad_sum(trainable_params(self.model), shard):
+            for s0, cnt in chunks(s_lo, s_hi, group):
+                host = None
+                if legacy is not None:
+                    host = legacy.chunk(s0, cnt)  # [cnt, n, *sp]
+                    if c > 1:  # the reference noises channel 0 only
+                        full = torch.zeros((cnt, n, c) + sp, dtype=torch.float32, device=dev)
+                        full[:, :, 0] = host
+                        host = full
+                if host is None and c == 1 and plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
+                    flat = plan.wavedec_noisy(x, sigma, cnt, n, 1, self.random_seed, s0)
+                else:
+                    noisy = noise_add(x, sigma, cnt, n, c * vol, vol, seed=self.random_seed, sample_base=s0,
+                                      host_noise=host)
+                    flat = plan.wavedec(noisy.view((cnt * n * c,) + sp))
+                cg = self._grads(plan, flat, cnt * n * c, y, cnt, n, c)
+                if shard.world == 1:
+                    self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 0, n_total=float(ns))
+                else:
+                    w = torch.from_numpy(legacy3d_weights(s0, cnt, ns)).to(dev)
+                    self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 1, weights=w)
+                self.wam._coeffs_src = (plan, flat, cnt * n * c, (cnt - 1) * n, n, c)
+                self.wam._coeffs = None
         if legacy is not None:
             legacy.finish()
         shard.all_reduce_sum(acc)
@@ -372,20 +366,21 @@ class WaveletAttribution3D(BaseWAM3D):
         group = 1 if y is None else auto_group(self.model, n, self.sample_batch, cap_items=32)
         acc = torch.zeros(n * S ** 3, dtype=torch.float32, device=dev)
         prev = torch.zeros_like(acc)
-        for k0, cnt in chunks(k_lo, k_hi, group):
-            img = plan.waverec(z, n * c, alphas=alphas[k0:k0 + cnt])
-            if y is None:
-                g = input_gradient(self.model, img.view((cnt * n, c) + plan.rec_shape).unsqueeze(0), None, 1, 1,
-                                   self.autocast_dtype, y_none_mean=True)[0]
-            else:
-                g = input_gradient(self.model, img.view((cnt * n, c) + plan.rec_shape), y, cnt, n,
-                                   self.autocast_dtype)
-            cg = plan.adjoint(g.reshape((cnt * n * c,) + plan.rec_shape))
-            if shard.world == 1:
-                self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 2, prev=prev, k0=k0)
-            else:
-                wk = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
-                self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 1, weights=wk)
+        with param_grad_sum(trainable_params(self.model), shard):
+            for k0, cnt in chunks(k_lo, k_hi, group):
+                img = plan.waverec(z, n * c, alphas=alphas[k0:k0 + cnt])
+                if y is None:
+                    g = input_gradient(self.model, img.view((cnt * n, c) + plan.rec_shape).unsqueeze(0), None, 1, 1,
+                                       self.autocast_dtype, y_none_mean=True)[0]
+                else:
+                    g = input_gradient(self.model, img.view((cnt * n, c) + plan.rec_shape), y, cnt, n,
+                                       self.autocast_dtype)
+                cg = plan.adjoint(g.reshape((cnt * n * c,) + plan.rec_shape))
+                if shard.world == 1:
+                    self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 2, prev=prev, k0=k0)
+                else:
+                    wk = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
+                    self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 1, weights=wk)
         shard.all_reduce_sum(acc)
         self._cube_dev = base.view(n, S, S, S) * acc.view(n, S, S, S)
         out = self._cube_dev.cpu().numpy()
