@@ -329,7 +329,8 @@ def test_noisy_haar3_equals_noise_then_wavedec(wam, shape, J, mode, S, N):
 
 @pytest.mark.parametrize("wav,shape,J,C", [("db4", (224, 224), 3, 3), ("haar", (224, 224), 3, 3),
                                            ("sym8", (128, 96), 2, 1), ("db6", (225, 223), 3, 3),
-                                           ("db2", (64, 300), 2, 1)])
+                                           ("db2", (64, 300), 2, 1), ("sym8", (512, 512), 5, 3),
+                                           ("db4", (300, 302), 3, 1)])
 def test_adjoint_maps_equals_adjoint_then_subband_maps(wam, wav, shape, J, C):
     p = wam.get_plan(2, shape, J, wav, "reflect", "cuda")
     assert p.caps & wam.CAP_ADJOINT_MAPS

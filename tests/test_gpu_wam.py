@@ -133,6 +133,45 @@ def test_philox_noise_statistics(W):
     assert not torch.equal(a[0], a[1])
 
 
+def test_philox_noise_distribution_1e8(W):
+    """The 'philox' noise stream over 1.0e8 draws (4 samples x 5 items x 5e6 elements, the
+    counters the fused kernels use): moments of N(0, 1) (mean, variance, skewness, excess
+    kurtosis within ~6 standard errors), a Kolmogorov-Smirnov bound against the normal CDF
+    (D_n * sqrt(n) < 1.95, p ~ 0.001), tail frequencies beyond 3 and 4 sigma, and no lag-1
+    correlation between neighbouring elements, items or samples."""
+    from wam_amd import plan as P
+    S, I, n = 4, 5, 5_000_000
+    x = torch.zeros(I, n, device="cuda")
+    z = P.noise_add(x, torch.ones(I, device="cuda"), S, I, n, n, seed=0x5EED_0001).view(S, I, n)
+    N = z.numel()
+    assert N >= 100_000_000
+    zd = z.double()
+    m = zd.mean().item()
+    c = zd - m
+    var = (c * c).mean().item()
+    skew = (c ** 3).mean().item() / var ** 1.5
+    kurt = (c ** 4).mean().item() / var ** 2 - 3.0
+    se = 1.0 / N ** 0.5
+    print("philox 1e8: mean %.2e var-1 %.2e skew %.2e kurt %.2e" % (m, var - 1, skew, kurt))
+    assert abs(m) < 6 * se and abs(var - 1) < 6 * 2 ** 0.5 * se
+    assert abs(skew) < 6 * 6 ** 0.5 * se and abs(kurt) < 6 * 24 ** 0.5 * se
+    del c, zd
+    srt = torch.sort(z.reshape(-1))[0].double()
+    cdf = torch.special.ndtr(srt)
+    k = torch.arange(1, N + 1, device="cuda", dtype=torch.float64) / N
+    d = torch.maximum((k - cdf).max(), (cdf - (k - 1.0 / N)).max()).item()
+    print("philox 1e8: KS D*sqrt(n) = %.3f" % (d * N ** 0.5))
+    assert d * N ** 0.5 < 1.95
+    del srt, cdf, k
+    for t, p in ((3.0, 2.6997960632601e-3), (4.0, 6.334248366623e-5)):
+        f = (z.abs() > t).double().mean().item()
+        assert abs(f - p) < 6 * (p * (1 - p) / N) ** 0.5, (t, f, p)
+    zf = z.float()
+    for a, b in ((zf[..., 1:], zf[..., :-1]), (zf[:, 1:], zf[:, :-1]), (zf[1:], zf[:-1])):
+        r = (a.double() * b.double()).mean().item()
+        assert abs(r) < 6 / a.numel() ** 0.5, r
+
+
 def test_philox_stream_matches_host_restatement(W):
     """The GPU noise stream is Philox4x32-10 (pinned by the Random123 known answers on the host
     restatement, tests/test_host_logic.py) + Box-Muller on the hardware transcendentals: compare

@@ -22,7 +22,7 @@
 // Boundary extension: map an extended-signal position to a source index (-1 = zero padding).
 // reflect / symmetric handle any number of reflections (pywt semantics; ptwt's torch 'reflect'
 // pad is the single-reflection special case).
-__device__ __forceinline__ int wam_ext_index(int i, int n, int mode) {
+__host__ __device__ __forceinline__ int wam_ext_index(int i, int n, int mode) {
   if (i >= 0 && i < n) return i;
   switch (mode) {
     case WAM_MODE_ZERO:

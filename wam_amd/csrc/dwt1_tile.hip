@@ -63,7 +63,7 @@ __host__ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v
 
 // boundary extension for indices at most one signal length outside [0, n) (the tile halos);
 // farther indices (tiny coarse levels) take the general rule
-__device__ __forceinline__ int ext_near(int i, int n, int mode) {
+__host__ __device__ __forceinline__ int ext_near(int i, int n, int mode) {
   if (i >= 0 && i < n) return i;
   int r;
   switch (mode) {
@@ -369,10 +369,16 @@ __host__ __device__ __forceinline__ int eo_cap(int n) { return (((n + 1) / 2 + 3
 // the S samples of a (signal, tile) read its window from one L2.
 constexpr int kPG = 6;  // noisy window: float4 groups per thread (window <= (kPG * kT1 - 1) * 4)
 
+// fold != 0: the units cover ALL tiles; the boundary tiles (outside [t_lo, t_hi)) take the same
+// closed-form ranges and fix the extension up where the signal ends: window slots whose source
+// index falls outside [0, n) are loaded through the boundary rule (noise keyed by the source
+// sample, as wam_noise_add noises the signal before it is extended), and after each level the
+// computed entries outside [0, m_l) are replaced by their extension (mirrors of computed entries,
+// host-checked) before the next level reads them; only own outputs inside [0, m_l) are stored.
 template <int L, bool NOISE>
 __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ in, float* __restrict__ coeffs,
                                                      const float* __restrict__ filt, Dwt1Geom g, int t_lo, int t_hi,
-                                                     int64_t units, WamNoise nz, int64_t S) {
+                                                     int64_t units, WamNoise nz, int64_t S, int fold) {
   constexpr int p = L - 2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
@@ -383,7 +389,8 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ 
     fhi[k] = filt[L + k];
   }
   const int J = g.J;
-  const int nti = t_hi - t_lo;
+  const int tbase = fold ? 0 : t_lo;
+  const int nti = fold ? g.tiles : t_hi - t_lo;
   const int tj = g.tile_j;
   const int n0 = (tj << (J - 1)) + p * ((1 << (J - 1)) - 1);  // level-0 computed outputs per tile
   const int wlen = 2 * n0 + p;
@@ -398,12 +405,12 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ 
   auto unit_geom = [&](int64_t u, int64_t& item, int64_t& src, int& tile, int& S0) {
     if constexpr (NOISE) {
       const int64_t s = u % S, rest = u / S, i = rest / nti;
-      tile = t_lo + (int)(rest - i * nti);
+      tile = tbase + (int)(rest - i * nti);
       src = i;
       item = s * nz.images + i;
     } else {
       item = src = u / nti;
-      tile = t_lo + (int)(u - item * nti);
+      tile = tbase + (int)(u - item * nti);
     }
     S0 = ((tile * tj) << (J - 1)) - p * ((1 << (J - 1)) - 1);
   };
@@ -417,21 +424,23 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ 
       // aligned groups [ga, gb) covering the window [w0, w0 + wlen); clamped to the last one
       const int w0 = 2 * S0 - p, ga = w0 >> 2, gb = (w0 + wlen + 3) >> 2;
       const float4* x4 = reinterpret_cast<const float4*>(in + src * (int64_t)g.n);
+      const int g_last = (g.n >> 2) - 1;  // boundary tiles: groups past the signal are clamped
 #pragma unroll
       for (int r = 0; r < kPG; ++r) {
         const int gi = ga + tid + r * kT1;
-        const float4 t = x4[gi < gb ? gi : gb - 1];
+        const float4 t = x4[min(max(gi < gb ? gi : gb - 1, 0), g_last)];
         pf[4 * r] = t.x;
         pf[4 * r + 1] = t.y;
         pf[4 * r + 2] = t.z;
         pf[4 * r + 3] = t.w;
       }
     } else {
-      const float* x = in + src * (int64_t)g.n + (2 * S0 - p);
+      const float* x = in + src * (int64_t)g.n;
+      const int w0 = 2 * S0 - p;
 #pragma unroll
       for (int r = 0; r < kPF; ++r) {
         const int j = tid + r * kT1;
-        pf[r] = x[j < wlen ? j : wlen - 1];
+        pf[r] = x[min(max(w0 + (j < wlen ? j : wlen - 1), 0), g.n - 1)];
       }
     }
   };
@@ -441,9 +450,11 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ 
     int64_t item, src;
     int tile, S0;
     unit_geom(u, item, src, tile, S0);
+    const int w0 = 2 * S0 - p;
+    const bool bnd = tile < t_lo || tile >= t_hi;  // (fold) a boundary tile: workgroup-uniform
     if constexpr (NOISE) {
       const NoiseItem ni = noise_item(nz, item);
-      const int w0 = 2 * S0 - p, ga = w0 >> 2, gb = (w0 + wlen + 3) >> 2;
+      const int ga = w0 >> 2, gb = (w0 + wlen + 3) >> 2;
 #pragma unroll
       for (int r = 0; r < kPG; r += 2) {
         const int gi0 = ga + tid + r * kT1, gi1 = gi0 + kT1;
@@ -452,17 +463,37 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ 
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int ja = 4 * gi0 + k - w0, jb = 4 * gi1 + k - w0;
-          if (gi0 < gb && ja >= 0 && ja < wlen)
+          // samples outside the signal (boundary tiles) come from the extension pass below
+          if (gi0 < gb && ja >= 0 && ja < wlen && (unsigned)(4 * gi0 + k) < (unsigned)g.n)
             ((ja & 1) ? winO : winE)[ja >> 1] = fmaf(ni.sg, za[k], pf[4 * r + k]);  // wam_noise_add's rounding
-          if (gi1 < gb && jb >= 0 && jb < wlen)
+          if (gi1 < gb && jb >= 0 && jb < wlen && (unsigned)(4 * gi1 + k) < (unsigned)g.n)
             ((jb & 1) ? winO : winE)[jb >> 1] = fmaf(ni.sg, zb[k], pf[4 * (r + 1) + k]);
+        }
+      }
+      if (bnd) {
+        const float* x = in + src * (int64_t)g.n;
+        for (int j = tid; j < wlen; j += kT1) {
+          const int gidx = w0 + j;
+          if ((unsigned)gidx < (unsigned)g.n) continue;
+          const int si = ext_near(gidx, g.n, g.mode);
+          const float v = si >= 0 ? fmaf(ni.sg, noise_at(si, ni.img, ni.smp, nz.k0, nz.k1), x[si]) : 0.f;
+          ((j & 1) ? winO : winE)[j >> 1] = v;
         }
       }
     } else {
 #pragma unroll
       for (int r = 0; r < kPF; ++r) {
         const int j = tid + r * kT1;
-        if (j < wlen) ((j & 1) ? winO : winE)[j >> 1] = pf[r];
+        if (j < wlen && (unsigned)(w0 + j) < (unsigned)g.n) ((j & 1) ? winO : winE)[j >> 1] = pf[r];
+      }
+      if (bnd) {
+        const float* x = in + src * (int64_t)g.n;
+        for (int j = tid; j < wlen; j += kT1) {
+          const int gidx = w0 + j;
+          if ((unsigned)gidx < (unsigned)g.n) continue;
+          const int si = ext_near(gidx, g.n, g.mode);
+          ((j & 1) ? winO : winE)[j >> 1] = si >= 0 ? x[si] : 0.f;
+        }
       }
     }
     __syncthreads();
@@ -505,7 +536,8 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ 
           D = __builtin_elementwise_fma((f2v)fhi[2 * m2 + 1], vo, D);
         }
         const int i = Sl + r;
-        const bool own_a = i >= own0 && i < own0 + T, own_b = i + 1 >= own0 && i + 1 < own0 + T && r + 1 < nl;
+        const bool own_a = i >= own0 && i < own0 + T && i < ml;
+        const bool own_b = i + 1 >= own0 && i + 1 < own0 + T && i + 1 < ml && r + 1 < nl;
         if (own_a && own_b && dpair) {
           *reinterpret_cast<float2*>(dout + i) = make_float2(D.x, D.y);
           if (last) *reinterpret_cast<float2*>(aout + i) = make_float2(A.x, A.y);
@@ -525,6 +557,19 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ 
         }
       }
       __syncthreads();
+      if (bnd && !last) {
+        // entries outside [0, m_l) become the level's extension (their mirrors are computed
+        // entries inside it, host-checked): the next level reads the extended approximation
+        for (int r = tid; r < nl; r += kT1) {
+          const int i = Sl + r;
+          if ((unsigned)i < (unsigned)ml) continue;
+          const int mi = ext_near(i, ml, g.mode);
+          const int rm = mi - Sl;
+          const float v = mi >= 0 ? ((rm & 1) ? oO : oE)[rm >> 1] : 0.f;
+          ((r & 1) ? oO : oE)[r >> 1] = v;
+        }
+        __syncthreads();
+      }
       iE = oE;
       iO = oO;
       Sl = (Sl + p) >> 1;
@@ -815,6 +860,27 @@ bool tile_interior(const Dwt1Geom& g, int tile, int p) {
   return true;
 }
 
+// boundary tiles can run in the interior kernel (fold): at every level but the last, each
+// computed entry outside [0, m_l) of a boundary tile's closed-form range mirrors to a zero or to a
+// computed entry inside [0, m_l)
+bool tiles_foldable(const Dwt1Geom& g, int p, int t_lo, int t_hi) {
+  for (int t = 0; t < g.tiles; ++t) {
+    if (t >= t_lo && t < t_hi) continue;
+    for (int l = 0; l + 1 < g.J; ++l) {
+      const int k = 1 << (g.J - 1 - l);
+      const int Sl = ((t * g.tile_j) * k) - p * (k - 1);
+      const int nl = g.tile_j * k + p * (k - 1);
+      const int ml = g.m[l];
+      for (int i = Sl; i < Sl + nl; ++i) {
+        if (i >= 0 && i < ml) continue;
+        const int mi = ext_near(i, ml, g.mode);
+        if (mi >= 0 && (mi < Sl || mi >= Sl + nl)) return false;
+      }
+    }
+  }
+  return true;
+}
+
 void interior_range(const Dwt1Geom& g, int p, int& t_lo, int& t_hi) {
   t_lo = t_hi = 0;
   int t = 0;
@@ -873,8 +939,11 @@ int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in,
   const int n0 = (g.tile_j << (g.J - 1)) + pp * ((1 << (g.J - 1)) - 1);
   const int lds_i = ana_int_lds_bytes(g, pp);
   if (2 * n0 + pp > kPF * kT1 || lds_i > kLds1Cap) t_lo = t_hi = 0;  // window too long: all tiles generic
-  const int64_t units = batch * (int64_t)(t_hi - t_lo);
-  const int64_t nb_blocks = batch * (int64_t)(g.tiles - (t_hi - t_lo));
+  // boundary tiles folded into the persistent launch (one launch, the interior kernel's level
+  // loop for every tile) when their extension stays within the closed-form ranges
+  const int fold = (t_hi > t_lo && tiles_foldable(g, pp, t_lo, t_hi)) ? 1 : 0;
+  const int64_t units = batch * (int64_t)(fold ? g.tiles : t_hi - t_lo);
+  const int64_t nb_blocks = fold ? 0 : batch * (int64_t)(g.tiles - (t_hi - t_lo));
   // algorithmic bytes: every input once (noisy: the clean signals once for all samples) and
   // every output once
   const double bytes = nz ? 4.0 * ((double)nz->images * n + (double)batch * p->band_off[p->nbands])
@@ -884,7 +953,8 @@ int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in,
     WAM_HIP_CHECK(hipGetDevice(&dev));
     int cus = 256;
     WAM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    WamTimer tm(st, nz ? "k_dwt1_ana_int<noise>" : "k_dwt1_ana_int", bytes * (double)(t_hi - t_lo) / g.tiles);
+    WamTimer tm(st, nz ? "k_dwt1_ana_int<noise>" : "k_dwt1_ana_int",
+                fold ? bytes : bytes * (double)(t_hi - t_lo) / g.tiles);
     // persistent grid: exactly the resident workgroups (VGPRs and LDS decide: 2 per CU for the
     // clean kernel's 107 VGPRs, 3 for the noisy one's 57 at c3's 51.5 KB of LDS), so no workgroup
     // waits for a slot and the units split evenly
@@ -896,7 +966,7 @@ int launch_dwt1_tile_analysis(const wam_plan* p, int64_t batch, const float* in,
     WAM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, k_dwt1_ana_int<LL, NN>, kT1, lds_i));         \
     const int64_t grid = std::min<int64_t>(units, (int64_t)std::max(1, wgs) * cus);                              \
     hipLaunchKernelGGL((k_dwt1_ana_int<LL, NN>), dim3((unsigned)grid), dim3(kT1), lds_i, st, in, coeffs, filt, g, \
-                       t_lo, t_hi, units, NZ, S);                                                                 \
+                       t_lo, t_hi, units, NZ, S, fold);                                                           \
   }
 #define WAM_D1AI(LL)                                                                                            \
   case LL:                                                                                                      \
