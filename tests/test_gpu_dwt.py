@@ -260,35 +260,6 @@ def test_noisy_wavedec_equals_noise_then_wavedec(wam, wav, J):
     assert torch.equal(fused, ref)
 
 
-@pytest.mark.parametrize("wav,shape,J,mode", [("db4", (224, 224), 3, "reflect"), ("db4", (224, 224), 1, "reflect"),
-                                              ("db3", (224, 224), 3, "symmetric"), ("db2", (224, 224), 2, "zero"),
-                                              ("db4", (100, 100), 3, "reflect"), ("sym4", (128, 96), 2, "reflect"),
-                                              ("coif1", (160, 224), 3, "constant"), ("db4", (60, 224), 2, "reflect")])
-def test_plane_halo_handoff_bit_identical(wam, wav, shape, J, mode):
-    """Wave chunks with the halo handed over between waves (default: each wave's first p/2 output
-    rows finished by the wave above from its ring and the published (lo, hi) rows) vs the
-    halo-refetch form (WAM_PLAN_NO_HANDOFF) and vs wam_noise_add + wavedec: the same taps in the
-    same fma order, so the noisy and the clean analyses are bit-identical (NO_COOP: wave chunks
-    for the clean analysis too)."""
-    hand = wam.get_plan(2, shape, J, wav, mode, "cuda", flags=wam.PLAN_NO_COOP)
-    refetch = wam.get_plan(2, shape, J, wav, mode, "cuda", flags=wam.PLAN_NO_COOP | wam.PLAN_NO_HANDOFF)
-    if not (hand.caps & wam.CAP_NOISY_WAVEDEC):
-        pytest.skip("plane kernels do not cover this geometry")
-    torch.manual_seed(17)
-    N, C, S = 3, 3, 5
-    item = C * shape[0] * shape[1]
-    x = torch.randn((N, C) + shape, device="cuda")
-    sigma = wam.item_sigma(x, item, item, 0.25)
-    a = hand.wavedec_noisy(x, sigma, S, N, C, seed=3, sample_base=1)
-    b = refetch.wavedec_noisy(x, sigma, S, N, C, seed=3, sample_base=1)
-    noisy = wam.noise_add(x, sigma, S, N, item, item, seed=3, sample_base=1)
-    c = refetch.wavedec(noisy.view(S * N * C, *shape))
-    assert torch.equal(a, b)
-    assert torch.equal(a, c)
-    xc = x.view(N * C, *shape)
-    assert torch.equal(hand.wavedec(xc), refetch.wavedec(xc))
-
-
 @pytest.mark.parametrize("n,J,wav,mode,S,N", [(80000, 5, "db6", "reflect", 3, 2), (9000, 5, "db6", "constant", 2, 3),
                                             (4096, 3, "haar", "symmetric", 4, 2), (1000, 4, "sym8", "zero", 2, 2),
                                             (40, 3, "db4", "reflect", 3, 1), (50000, 4, "coif2", "reflect", 2, 2)])

@@ -53,14 +53,6 @@ struct PlaneGeom {
   int sample_fast;                  // noisy analysis: logical order sample-fastest (1) or plane-fastest (0)
   int xcd_order;                    // workgroup ids through the XCD-aware swizzle (1) or as issued (0)
   int coop;                         // level 1 as the cooperative row stream (COOP kernels)
-  // wave chunks with halo handoff (handoff != 0): wave w owns output rows [cst[w], cst[w+1]);
-  // waves w >= 1 start at their own first ext row and leave their first p/2 output rows to wave
-  // w - 1, which finishes them after its last row from its register ring plus the p ext rows
-  // (horizontal (lo, hi)) wave w published to hs after its prologue -- no halo row is fetched,
-  // noised or filtered twice
-  int handoff;
-  int cst[kPW + 1];
-  float* hs;                        // [items][kPW][p][mw] float2 handoff rows (plan workspace)
 };
 
 template <bool MAPS>
@@ -364,23 +356,11 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     const bool zero_mode = mode == WAM_MODE_ZERO;
     const PadLane pl = pad_lane(lane, nw, p, mode);
     if (zero_mode && pl.dst >= 0) lds[pl.dst] = 0.f;
-    constexpr int D = p / 2;           // output rows whose taps reach p ext rows above a chunk
-    const bool hand = g.handoff != 0;
-    int i0, i1;
-    if (hand) {
-      i0 = g.cst[wv];
-      i1 = g.cst[wv + 1];
-    } else {
-      const int R = (mh + kPW - 1) / kPW;
-      i0 = wv * R;
-      i1 = min(mh, i0 + R);
-    }
-    // handoff: waves >= 1 emit from ie = i0 + D on (their first D rows are finished by wave - 1),
-    // so their ext rows start at their own first row 2 i0 (no halo above)
-    const bool defer = hand && wv > 0;
-    const int ie = defer ? i0 + D : i0;
-    const int er0 = 2 * ie - p;
-    const int T = i1 > ie ? 2 * (i1 - ie) + L - 2 : 0;
+    const int R = (mh + kPW - 1) / kPW;
+    const int i0 = wv * R;
+    const int i1 = min(mh, i0 + R);
+    const int er0 = 2 * i0 - p;
+    const int T = i1 > i0 ? 2 * (i1 - i0) + L - 2 : 0;
     float mx[4] = {0.f, 0.f, 0.f, 0.f};
     const float2* hsrc[CPL];
 #pragma unroll
@@ -471,38 +451,20 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     // Every fetch is unconditional (rows past the chunk are clamped to valid source rows and never
     // emitted): loads under divergent control flow would make the compiler drain vmcnt to 0 at the
     // join, serialising the row stream on memory latency.
-    float za[4] = {0.f, 0.f, 0.f, 0.f}, zb[4] = {0.f, 0.f, 0.f, 0.f};
     if (T > 0) {
 #pragma unroll
       for (int u = 0; u < NBL - 1; ++u) fetch(f[u], srow[u], u);
       // prologue: ext rows 0 .. L-3 fill ring slots 0 .. L-3
+      float za[4] = {0.f, 0.f, 0.f, 0.f}, zb[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < L - 2; ++t) {
         fetch(f[(t + NBL - 1) % NBL], srow[(t + NBL - 1) % NBL], t + NBL - 1);
         if (!(t & 1)) noise2(za, zb, srow[t % NBL], srow[(t + 1) % NBL]);  // row t + 1 is fetched
         consume(f[t % NBL], srow[t % NBL], t, (t & 1) ? zb : za);
       }
-    }
-    if (hand) {
-      // publish this chunk's first p ext rows (ring slots 0 .. p-1) for the wave above; one
-      // workgroup barrier (every wave, right after its p-row prologue) orders them before the
-      // reads in the fix-up below
-      if (defer && T > 0) {
-        float2* hb = reinterpret_cast<float2*>(g.hs) + (item * kPW + wv) * (int64_t)p * mw;
-#pragma unroll
-        for (int t = 0; t < p; ++t)
-#pragma unroll
-          for (int c = 0; c < CPL; ++c) {
-            const int j = lane + 64 * c;
-            if (j < mw) hb[t * mw + j] = make_float2(rv[c][t].x, rv[c][t].y);
-          }
-      }
-      __syncthreads();
-    }
-    if (T > 0) {
       // steady state: GRPL ext rows per iteration; t = base + u with base = L-2 (mod GRPL), so
       // t % L and t % NBL are compile-time constants; a partial last group computes output rows
-      // >= i1, which emit() drops (handoff chunks end on a whole group: T - p = 0 mod GRPL)
+      // >= i1, which emit() drops
       for (int base = L - 2; base < T; base += GRPL) {
 #pragma unroll
         for (int u = 0; u < GRPL; ++u) {
@@ -512,50 +474,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
             noise2(za, zb, srow[(L - 2 + u) % NBL], srow[(L - 2 + u + 1) % NBL]);
           consume(f[(L - 2 + u) % NBL], srow[(L - 2 + u) % NBL], (L - 2 + u) % L, (u & 1) ? zb : za);
           // after odd u: output row (t - (L-1)) / 2 from ext rows t-L+1 .. t = slots (u-1+k) % L
-          if (u & 1) emit(ie + (t - (L - 1)) / 2, (u - 1) % L);
-        }
-      }
-    }
-    if (hand && wv + 1 < kPW && T > 0) {
-      // the first D output rows of the chunk below: ext rows 2 il - p .. 2 il - 1 are this
-      // wave's last p rows (ring slots 0 .. p-1: T - p = 0 mod L), ext rows 2 il .. 2 il + p - 1
-      // the lower wave's published rows; each output keeps emit()'s tap order (same sums)
-      const int il = g.cst[wv + 1], il1 = g.cst[wv + 2];
-      const float2* hb = reinterpret_cast<const float2*>(g.hs) + (item * kPW + wv + 1) * (int64_t)p * mw;
-      f2 low[CPL][p > 0 ? p : 1];
-#pragma unroll
-      for (int q = 0; q < p; ++q)
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          const float2 v = hb[q * mw + min(lane + 64 * c, mw - 1)];
-          low[c][q] = f2{v.x, v.y};
-        }
-#pragma unroll
-      for (int m = 0; m < D; ++m) {
-        const int i = il + m;
-        f2 av[CPL], hd[CPL];
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) av[c] = hd[c] = f2{0.f, 0.f};
-#pragma unroll
-        for (int k = 0; k < L; ++k) {
-#pragma unroll
-          for (int c = 0; c < CPL; ++c) {
-            const f2 r = (2 * m + k < p) ? rv[c][2 * m + k] : low[c][2 * m + k - p];
-            av[c] = __builtin_elementwise_fma(f2{fh2[k].x, fh2[k].x}, r, av[c]);
-            hd[c] = __builtin_elementwise_fma(f2{fh2[k].y, fh2[k].y}, r, hd[c]);
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          const int j = lane + 64 * c;
-          if (j < mw && i < il1) {
-            const int64_t idx = (int64_t)i * mw + j;
-            if (lastlvl) bo.put(g, g.off_a, bn, idx, av[c].x, mx[3]);
-            else bufA[idx] = av[c].x;
-            bo.put(g, g.off[0][0], bn, idx, hd[c].x, mx[0]);
-            bo.put(g, g.off[0][1], bn, idx, av[c].y, mx[1]);
-            bo.put(g, g.off[0][2], bn, idx, hd[c].y, mx[2]);
-          }
+          if (u & 1) emit(i0 + (t - (L - 1)) / 2, (u - 1) % L);
         }
       }
     }
@@ -850,37 +769,6 @@ PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items
   return g;
 }
 
-// Halo handoff chunks for the wave-chunk form (single-plane items): wave 0 owns u*k output rows,
-// waves 1 .. kPW-2 own D + u*k (D = p / 2 deferred rows finished by the wave above, then whole
-// loop groups of u = GRPL / 2 rows, so every upper wave's ring ends on slot p - 1), the last wave
-// the rest (at least D + 1). Equal ext rows per wave: 2 u k + p. false: no such split (the
-// halo-refetch form is used).
-bool handoff_chunks(int mh, int L, int mw, int cst[kPW + 1]) {
-  const int p = L - 2, D = p / 2;
-  if (p == 0) return false;
-  const int cpl = mw > 64 ? 2 : 1;
-  const int nbl = cpl > 1 ? 2 : 4;  // k_plane_ana's NBL for single-plane items
-  int a = L, b = nbl;
-  while (b) {
-    const int t = a % b;
-    a = b;
-    b = t;
-  }
-  const int u = L / a * nbl / 2;  // lcm(L, NBL) / 2 output rows per loop group
-  for (int k = 1;; ++k) {
-    const int r0 = u * k, rm = D + u * k;
-    const int rl = mh - r0 - (kPW - 2) * rm;
-    if (rl < D + 1) return false;
-    if (rl <= rm + u) {
-      cst[0] = 0;
-      cst[1] = r0;
-      for (int w = 2; w < kPW; ++w) cst[w] = cst[w - 1] + rm;
-      cst[kPW] = mh;
-      return true;
-    }
-  }
-}
-
 template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP>
 int launch_plane_t(const PlaneGeom& g, int lds_bytes, int64_t n_items, const float* in, float* out, float* band_max,
                    const float* filt, const WamNoise& nz, int64_t S, int64_t group_items, const char* name,
@@ -932,21 +820,13 @@ bool dwt2_plane_supported(const wam_plan* p, bool adjoint) {
 }
 
 int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in, float* coeffs, bool adjoint,
-                               const WamNoise* nz, int64_t n_samples, hipStream_t st, void* ws, int64_t ws_bytes) {
+                               const WamNoise* nz, int64_t n_samples, hipStream_t st) {
   if (((uintptr_t)in & 15) || !dwt2_plane_supported(p, adjoint)) return WAM_ERR_UNSUPPORTED;
   const int nh0 = (int)(adjoint ? p->rec_shape[0] : p->lin[0][0]);
   const int nw0 = (int)(adjoint ? p->rec_shape[1] : p->lin[0][1]);
   const int mode = adjoint ? WAM_MODE_ZERO : p->mode;
   const float* filt = p->d_filt + (adjoint ? WAM_F_ADJ_LO : WAM_F_ANA_LO) * p->L;
-  PlaneGeom g = make_geom(p, nh0, nw0, mode, items, nz != nullptr);
-  // the wave-chunk form hands its halo rows over instead of refetching and re-noising them when
-  // the chunks split evenly and the plan workspace holds the handoff rows
-  if (!g.coop && ws && !(p->flags & WAM_PLAN_NO_HANDOFF) &&
-      handoff_chunks(g.mh[0], p->L, g.mw[0], g.cst) &&
-      items * kPW * (int64_t)(p->L - 2) * g.mw[0] * 8 <= ws_bytes) {
-    g.handoff = 1;
-    g.hs = (float*)ws;
-  }
+  const PlaneGeom g = make_geom(p, nh0, nw0, mode, items, nz != nullptr);
   int rowlds, llcap;
   const int lds_bytes = lds_floats(p, nw0, rowlds, llcap, nz != nullptr) * 4;
   const double in_planes = nz ? (double)nz->images * nz->channels : (double)items;

@@ -64,8 +64,7 @@ struct WamNoise {
 // plane-resident multi-level 2D analysis (dwt2_plane.hip): all levels of a plane in one workgroup
 bool dwt2_plane_supported(const wam_plan* p, bool adjoint);
 int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in, float* coeffs, bool adjoint,
-                               const WamNoise* nz, int64_t n_samples, hipStream_t st,
-                               void* ws = nullptr, int64_t ws_bytes = 0);
+                               const WamNoise* nz, int64_t n_samples, hipStream_t st);
 int launch_dwt2_plane_maps(const wam_plan* p, int64_t images, int channels, int64_t group_items, const float* grad,
                            float* maps, float* band_max, hipStream_t st);
 bool dwt2_plane_syn_supported(const wam_plan* p);

@@ -364,8 +364,7 @@ bool use_colstrip(const wam_plan* p) {
 int analysis_driver(const wam_plan* p, int64_t batch, const float* x, float* coeffs, void* ws, hipStream_t st,
                     bool adjoint, const WamNoise* noise = nullptr, int64_t n_samples = 1) {
   if (use_plane(p, adjoint)) {  // all levels in one launch, LL pyramid in LDS
-    int rc = launch_dwt2_plane_analysis(p, batch, x, coeffs, adjoint, noise, n_samples, st, ws,
-                                        wam_plan_workspace_bytes(p, batch));
+    int rc = launch_dwt2_plane_analysis(p, batch, x, coeffs, adjoint, noise, n_samples, st);
     if (rc != WAM_ERR_UNSUPPORTED) return rc;
   }
   if (p->ndim == 1 && !(p->flags & WAM_PLAN_GENERIC)) {  // all levels per signal tile
