@@ -809,6 +809,7 @@ def main():
     if world > 1:
         log("collectives timing")
         secondary["collectives"] = collectives_timing(wl, dev, world, axis)
+    if world > 1 and args.extras == "auto":
         log("weak scaling: each rank its own %d-item batch" % wl.n)
         exw = build_explainer(wl, dev, args, dist_on=False)  # each rank its own batch, no collective
         dtw, _, _ = timed(lambda: exw(xd, y), 2, 1, world, dev)
