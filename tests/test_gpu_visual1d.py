@@ -100,6 +100,12 @@ def test_compute_spectrogram_nnls(W, sr, n_fft, n_mels, T):
         assert err <= 1e-4 and fo <= fe * (1 + 1e-5) + 1e-12 * np.sum(B ** 2), (i, err, fo, fe)
         ref, _ = om.mel_to_stft(mel[i], sr, n_fft)
         assert fo <= _nnls_obj(A, ref.astype(np.float64) ** 2, B) * (1 + 1e-6)
+        # the returned magnitudes themselves: a different point of the NNLS solution set than
+        # librosa's early-stopped L-BFGS-B iterate (reported, not bounded: ADVICE r03)
+        gap = np.abs(spec[i] - ref).max() / max(1e-30, np.abs(ref).max())
+        rgap = np.abs(A @ (ref.astype(np.float64) ** 2) - A @ xe).max() / np.abs(B).max()
+        print("compute_spectrogram vs librosa-restated L-BFGS-B: max |x gap| %.3e of max |x|, "
+              "re-projection gaps: device %.2e, L-BFGS-B %.2e of max |B|" % (gap, err, rgap))
     # process_in_chunks (module function, lib/wam_1D.py:442-448): the same per-frame inversion in
     # chunks of 5 frames. The minimiser is not unique (more bins than bands) and the solver stops on
     # the worst column of a chunk, so chunkings agree on the re-projection A x (unique), not on x

@@ -26,7 +26,9 @@ def process_in_chunks(melspec, chunk_size, sr, n_fft):
     """lib/wam_1D.py:442-448: librosa.feature.inverse.mel_to_stft of a [n_mels, T] power mel
     spectrogram in time chunks of chunk_size frames -> [1 + n_fft // 2, T] magnitudes. The device
     NNLS (wam_amd.melspec.mel_to_stft) solves every frame independently, so the chunks are one
-    batch here; chunk_size only keeps the reference's signature."""
+    batch here; chunk_size only keeps the reference's signature. Returns the exact NNLS minimiser:
+    it matches librosa's L-BFGS-B result in the re-projected mel spectrogram, not necessarily in the
+    magnitudes (see VisualizerWAM1D.compute_spectrogram)."""
     from .melspec import mel_to_stft
     if int(chunk_size) < 1:
         raise ValueError("range() arg 3 must not be zero")
@@ -322,7 +324,14 @@ class VisualizerWAM1D(WaveletAttribution1D):
     def compute_spectrogram(self, melspecs, chunk_size=100):
         """lib/wam_1D.py:478-488: the STFT magnitudes of power mel spectrograms [N, n_mels, T] by
         librosa.feature.inverse.mel_to_stft (NNLS on librosa's Slaney mel basis, then sqrt), all
-        waveforms and frames in one device batch -> [N, 1 + n_fft // 2, T] float32."""
+        waveforms and frames in one device batch -> [N, 1 + n_fft // 2, T] float32.
+
+        The result is the exact NNLS minimiser (FISTA run to a KKT tolerance), not librosa's
+        L-BFGS-B iterate, which stops early at an absolute projected-gradient tolerance. The mel
+        basis has more bins than bands, so the minimiser is not unique: only the re-projected mel
+        spectrogram A x (and the objective) match librosa's; the magnitudes themselves can differ
+        in the basis' null space (tests/test_gpu_visual1d.py reports the gap). chunk_size is
+        validated and otherwise unused: every frame is solved on its own."""
         from .melspec import mel_to_stft
         if int(chunk_size) < 1:
             raise ValueError("range() arg 3 must not be zero")
