@@ -16,7 +16,7 @@ rc=$?
 KT=$(find /tmp/trace_$CFG -name "*kernel_trace.csv" | head -1)
 KS=$(find /tmp/trace_$CFG -name "*kernel_stats.csv" | head -1)
 [ -n "$KS" ] && cp "$KS" $O/kernel_stats.csv
-[ -n "$KT" ] && python3 $R/scripts/trace_window.py "$KT" $WIN > $O/window.txt
+[ -n "$KT" ] && python3 $R/scripts/trace_window.py "$KT" $WIN $O/kernel_stats_window.csv > $O/window.txt
 rm -rf /tmp/trace_$CFG
 tail -3 $O/bench.log
 exit $rc
