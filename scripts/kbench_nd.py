@@ -29,6 +29,12 @@ def main():
         if args.only and not tag.startswith(args.only):
             continue
         p = P.get_plan(dim, shape, J, wav, mode, "cuda")
+        if dim == 1:  # the c3 bench's noisy group: 256 clips x 5 samples per launch
+            xc = torch.randn(256, shape[0], device="cuda")
+            sig = P.item_sigma(xc, shape[0], shape[0], 0.25)
+            run(f"{tag} wavedec_noisy 256x5", lambda: p.wavedec_noisy(xc, sig, 5, 256, 1, seed=1, sample_base=0),
+                args.iters)
+            del xc
         x = torch.randn((B,) + shape, device="cuda")
         run(f"{tag} wavedec B={B}", lambda: p.wavedec(x), args.iters)
         cf = p.wavedec(x)

@@ -455,20 +455,35 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ 
     if constexpr (NOISE) {
       const NoiseItem ni = noise_item(nz, item);
       const int ga = w0 >> 2, gb = (w0 + wlen + 3) >> 2;
+      // a group inside both the window and the signal lands whole: w0 is even (L is), so its
+      // samples k = 0, 2 go to E[h], E[h + 1] and k = 1, 3 to O[h], O[h + 1] (h = (4 gi - w0) / 2);
+      // the groups at the window's ends and past the signal take the per-sample checks
+      auto commit = [&](int gi, const float* z, const float* x4) {
+        const int j0 = 4 * gi - w0;
+        if (gi >= 0 && j0 >= 0 && j0 + 4 <= wlen && 4 * gi + 4 <= g.n) {
+          const int h = j0 >> 1;
+          winE[h] = fmaf(ni.sg, z[0], x4[0]);  // wam_noise_add's rounding
+          winO[h] = fmaf(ni.sg, z[1], x4[1]);
+          winE[h + 1] = fmaf(ni.sg, z[2], x4[2]);
+          winO[h + 1] = fmaf(ni.sg, z[3], x4[3]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int j = j0 + k;
+            // samples outside the signal (boundary tiles) come from the extension pass below
+            if (gi < gb && j >= 0 && j < wlen && (unsigned)(4 * gi + k) < (unsigned)g.n)
+              ((j & 1) ? winO : winE)[j >> 1] = fmaf(ni.sg, z[k], x4[k]);
+          }
+        }
+      };
 #pragma unroll
       for (int r = 0; r < kPG; r += 2) {
         const int gi0 = ga + tid + r * kT1, gi1 = gi0 + kT1;
+        if (gi0 >= gb) continue;  // whole waves past the window skip the pair's Philox blocks
         float za[4], zb[4];
         wam_normal4_x2((uint32_t)gi0, (uint32_t)gi1, ni.img, ni.smp, nz.k0, nz.k1, za, zb);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int ja = 4 * gi0 + k - w0, jb = 4 * gi1 + k - w0;
-          // samples outside the signal (boundary tiles) come from the extension pass below
-          if (gi0 < gb && ja >= 0 && ja < wlen && (unsigned)(4 * gi0 + k) < (unsigned)g.n)
-            ((ja & 1) ? winO : winE)[ja >> 1] = fmaf(ni.sg, za[k], pf[4 * r + k]);  // wam_noise_add's rounding
-          if (gi1 < gb && jb >= 0 && jb < wlen && (unsigned)(4 * gi1 + k) < (unsigned)g.n)
-            ((jb & 1) ? winO : winE)[jb >> 1] = fmaf(ni.sg, zb[k], pf[4 * (r + 1) + k]);
-        }
+        commit(gi0, za, pf + 4 * r);
+        if (gi1 < gb) commit(gi1, zb, pf + 4 * (r + 1));
       }
       if (bnd) {
         const float* x = in + src * (int64_t)g.n;
