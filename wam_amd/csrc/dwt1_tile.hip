@@ -530,6 +530,9 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ 
       // lo / hi sums as packed fp32 fma (per-output tap order unchanged)
       constexpr int H2 = L / 2, NP = H2 / 2 + 1;
       const bool dpair = ((reinterpret_cast<uintptr_t>(dout + Sl) | reinterpret_cast<uintptr_t>(aout + Sl)) & 7) == 0;
+      // own outputs: i in [own0, oend) (the tile's range, the level's length and the computed range)
+      const int oend = min(min(own0 + T, ml), Sl + nl);
+      const unsigned ospan = (unsigned)max(oend - own0, 0);
       for (int r = 2 * tid; r < nl; r += 2 * kT1) {
         float e[2 * NP], o[2 * NP];
 #pragma unroll
@@ -541,18 +544,21 @@ __global__ void __launch_bounds__(kT1) k_dwt1_ana_int(const float* __restrict__ 
           o[2 * k] = to.x;
           o[2 * k + 1] = to.y;
         }
-        f2v A = {0.f, 0.f}, D = {0.f, 0.f};
+        // packed as (lo, hi) tap pairs times a broadcast sample: each operand is one element of a
+        // loaded pair (op_sel), no register moves to build straddling (E[r + m], E[r + m + 1]) pairs
+        f2v P0 = {0.f, 0.f}, P1 = {0.f, 0.f};  // (a, d) of outputs r and r + 1
 #pragma unroll
         for (int m2 = 0; m2 < H2; ++m2) {
-          const f2v ve = {e[m2], e[m2 + 1]}, vo = {o[m2], o[m2 + 1]};
-          A = __builtin_elementwise_fma((f2v)flo[2 * m2], ve, A);
-          D = __builtin_elementwise_fma((f2v)fhi[2 * m2], ve, D);
-          A = __builtin_elementwise_fma((f2v)flo[2 * m2 + 1], vo, A);
-          D = __builtin_elementwise_fma((f2v)fhi[2 * m2 + 1], vo, D);
+          const f2v k0 = {flo[2 * m2], fhi[2 * m2]}, k1 = {flo[2 * m2 + 1], fhi[2 * m2 + 1]};
+          P0 = __builtin_elementwise_fma(k0, (f2v)e[m2], P0);
+          P1 = __builtin_elementwise_fma(k0, (f2v)e[m2 + 1], P1);
+          P0 = __builtin_elementwise_fma(k1, (f2v)o[m2], P0);
+          P1 = __builtin_elementwise_fma(k1, (f2v)o[m2 + 1], P1);
         }
+        const f2v A = {P0.x, P1.x}, D = {P0.y, P1.y};
         const int i = Sl + r;
-        const bool own_a = i >= own0 && i < own0 + T && i < ml;
-        const bool own_b = i + 1 >= own0 && i + 1 < own0 + T && i + 1 < ml && r + 1 < nl;
+        const bool own_a = (unsigned)(i - own0) < ospan;
+        const bool own_b = (unsigned)(i + 1 - own0) < ospan;
         if (own_a && own_b && dpair) {
           *reinterpret_cast<float2*>(dout + i) = make_float2(D.x, D.y);
           if (last) *reinterpret_cast<float2*>(aout + i) = make_float2(A.x, A.y);
