@@ -789,15 +789,16 @@ __global__ void __launch_bounds__(kT1) k_dwt1_syn_int(const float* __restrict__ 
       // outputs past the approximation's band (or the signal) are zeros / not written
       const int vout = ll ? g.m[ll > 0 ? ll - 1 : 0] - (u0 >> ll) : nout0 - u0;
       for (int q = tid; q < (NOUT + 1) / 2; q += kT1) {
-        float ya = 0.f, yb = 0.f;
+        // (ya, yb) as one packed chain: tap pairs (2j, 2j + 1) times the broadcast coefficient,
+        // each output keeping the scalar chain's tap order (same sums)
+        f2v y = {0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < H2; ++j) {
           const float av = ain[q + H2 - 1 - j], dv = din[q + H2 - 1 - j];
-          ya = fmaf(rlo[2 * j], av, ya);
-          ya = fmaf(rhi[2 * j], dv, ya);
-          yb = fmaf(rlo[2 * j + 1], av, yb);
-          yb = fmaf(rhi[2 * j + 1], dv, yb);
+          y = __builtin_elementwise_fma(f2v{rlo[2 * j], rlo[2 * j + 1]}, (f2v)av, y);
+          y = __builtin_elementwise_fma(f2v{rhi[2 * j], rhi[2 * j + 1]}, (f2v)dv, y);
         }
+        const float ya = y.x, yb = y.y;
         if (ll) {
           aout[2 * q] = 2 * q < vout ? ya : 0.f;
           if (NOUT % 2 == 0 || 2 * q + 1 < NOUT) aout[2 * q + 1] = 2 * q + 1 < vout ? yb : 0.f;
