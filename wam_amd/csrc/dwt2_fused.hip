@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(256) k_dwt2_ana(const float* __restrict__ in, 
   constexpr int SEGW = 128 + L - 2;
   __shared__ __attribute__((aligned(16))) float seg[4][SEGW + 2];
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR bases
   const int64_t gw = wam_xcd_block(blockIdx.x, gridDim.x) * 4 + wv;
   if (gw >= total_waves) return;
   // strip fastest: the strips of one (plane, row chunk) -- which fetch the same source rows --
@@ -130,7 +130,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L <= 1
                                                   int nchunks, int RQ, int64_t total_waves) {
   __shared__ __attribute__((aligned(16))) float4 xch[4][64];
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR bases
   const int64_t gw = wam_xcd_block(blockIdx.x, gridDim.x) * 4 + wv;
   if (gw >= total_waves) return;
   // strip fastest, then alpha: the strips of one (plane, row chunk) -- which fetch the same source

@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, 
   constexpr int p = L - 2;
   __shared__ __attribute__((aligned(16))) float rows[kWaves][kRowLds];
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR bases
   const int64_t gw = wam_xcd_block(blockIdx.x, gridDim.x) * kWaves + wv;
   if (gw >= total_waves) return;
   // strip fastest: the strips of one (plane, row chunk) -- which fetch the same source rows --
@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
   constexpr int p = L - 2;
   __shared__ __attribute__((aligned(16))) float rows[kWaves][C][kRowLds];
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR bases
   const int64_t gw = wam_xcd_block(blockIdx.x, gridDim.x) * kWaves + wv;
   if (gw >= total_waves) return;
   // strip fastest: the strips of one (plane, row chunk) -- which fetch the same source rows --

@@ -158,6 +158,15 @@ __device__ __forceinline__ wam_f2 hfilter_pk(const float* lds, int j, int p, con
 // vec2: output row bases are 8-byte aligned (pairs stored as float2).
 constexpr int kSynPF = 4;
 
+// base[idx] with a 32-bit byte offset: a wave-uniform base stays in SGPRs and the access is one
+// global load / store with an SGPR base and a VGPR offset (no 64-bit address arithmetic)
+__device__ __forceinline__ const float* at32(const float* base, unsigned idx) {
+  return reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + idx * 4u);
+}
+__device__ __forceinline__ float* at32(float* base, unsigned idx) {
+  return reinterpret_cast<float*>(reinterpret_cast<char*>(base) + idx * 4u);
+}
+
 constexpr int syn_gcd(int a, int b) { return b == 0 ? a : syn_gcd(b, a % b); }
 constexpr int syn_lcm(int a, int b) { return a / syn_gcd(a, b) * b; }
 
@@ -196,11 +205,13 @@ __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float s
   bool fok[PF];
   auto fetch = [&](int u, int q) {
     fok[u] = colv && q >= 0 && q < mh;
-    const int o = min(max(q, 0), mh - 1) * mw + jc;
-    fa[u] = pA[o];
-    fh[u] = pH[o];
-    fv[u] = pV[o];
-    fd[u] = pD[o];
+    // unsigned 32-bit element offsets from the (wave-uniform) band bases: SGPR-base loads, no
+    // 64-bit address arithmetic per row
+    const unsigned o = (unsigned)(min(max(q, 0), mh - 1) * mw + jc);
+    fa[u] = *at32(pA, o);
+    fh[u] = *at32(pH, o);
+    fv[u] = *at32(pV, o);
+    fd[u] = *at32(pD, o);
   };
   if constexpr (PK) {
     // filter pairs (taps 2 i2, 2 i2 + 1): the two outputs of a phase pair as one (packed) chain
@@ -263,7 +274,7 @@ __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float s
           if (ucol >= 0 && ucol < ow) {
             const bool two = ucol + 1 < ow, pair = two && vec2;
             if (r0 < oh) {
-              float* d0 = dst + (int64_t)r0 * ow + ucol;
+              float* d0 = at32(dst, (unsigned)(r0 * ow + ucol));
               if (pair) {
                 *reinterpret_cast<float2*>(d0) = make_float2(o0.x, o0.y);
               } else {
@@ -272,7 +283,7 @@ __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float s
               }
             }
             if (r0 + 1 < oh) {
-              float* d1 = dst + (int64_t)(r0 + 1) * ow + ucol;
+              float* d1 = at32(dst, (unsigned)((r0 + 1) * ow + ucol));
               if (pair) {
                 *reinterpret_cast<float2*>(d1) = make_float2(o1.x, o1.y);
               } else {
@@ -339,7 +350,7 @@ __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float s
           if (ucol >= 0 && ucol < ow) {
             const bool two = ucol + 1 < ow, pair = two && vec2;
             if (r0 < oh) {
-              float* d0 = dst + (int64_t)r0 * ow + ucol;
+              float* d0 = at32(dst, (unsigned)(r0 * ow + ucol));
               if (pair) {
                 *reinterpret_cast<float2*>(d0) = make_float2(o00, o01);
               } else {
@@ -348,7 +359,7 @@ __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float s
               }
             }
             if (r0 + 1 < oh) {
-              float* d1 = dst + (int64_t)(r0 + 1) * ow + ucol;
+              float* d1 = at32(dst, (unsigned)((r0 + 1) * ow + ucol));
               if (pair) {
                 *reinterpret_cast<float2*>(d1) = make_float2(o10, o11);
               } else {
