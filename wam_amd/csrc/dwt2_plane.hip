@@ -640,7 +640,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
   const int64_t q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
   const int64_t lwg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
   if (lwg >= n_items) return;  // never taken (grid == n_items)
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   // alpha-fastest: the alphas of one plane share an XCD and its coefficient reads
   const int64_t item = lwg / g.n_alpha;
   const int ai = (int)(lwg % g.n_alpha);

@@ -273,22 +273,30 @@ __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float s
           const int r0 = 2 * (q - qs);
           if (ucol >= 0 && ucol < ow) {
             const bool two = ucol + 1 < ow, pair = two && vec2;
-            if (r0 < oh) {
-              float* d0 = at32(dst, (unsigned)(r0 * ow + ucol));
-              if (pair) {
-                *reinterpret_cast<float2*>(d0) = make_float2(o0.x, o0.y);
-              } else {
-                d0[0] = o0.x;
-                if (two) d0[1] = o0.y;
+            if (pair && r0 + 1 < oh) {
+              // the common case in one block: both chains are used by it, so the compiler keeps
+              // them interleaved (with a store branch per row it sank each 2 H2-deep dependent
+              // chain into its own branch, back to back)
+              *reinterpret_cast<float2*>(at32(dst, (unsigned)(r0 * ow + ucol))) = make_float2(o0.x, o0.y);
+              *reinterpret_cast<float2*>(at32(dst, (unsigned)((r0 + 1) * ow + ucol))) = make_float2(o1.x, o1.y);
+            } else {
+              if (r0 < oh) {
+                float* d0 = at32(dst, (unsigned)(r0 * ow + ucol));
+                if (pair) {
+                  *reinterpret_cast<float2*>(d0) = make_float2(o0.x, o0.y);
+                } else {
+                  d0[0] = o0.x;
+                  if (two) d0[1] = o0.y;
+                }
               }
-            }
-            if (r0 + 1 < oh) {
-              float* d1 = at32(dst, (unsigned)((r0 + 1) * ow + ucol));
-              if (pair) {
-                *reinterpret_cast<float2*>(d1) = make_float2(o1.x, o1.y);
-              } else {
-                d1[0] = o1.x;
-                if (two) d1[1] = o1.y;
+              if (r0 + 1 < oh) {
+                float* d1 = at32(dst, (unsigned)((r0 + 1) * ow + ucol));
+                if (pair) {
+                  *reinterpret_cast<float2*>(d1) = make_float2(o1.x, o1.y);
+                } else {
+                  d1[0] = o1.x;
+                  if (two) d1[1] = o1.y;
+                }
               }
             }
           }
@@ -349,22 +357,27 @@ __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float s
           const int r0 = 2 * (q - qs);
           if (ucol >= 0 && ucol < ow) {
             const bool two = ucol + 1 < ow, pair = two && vec2;
-            if (r0 < oh) {
-              float* d0 = at32(dst, (unsigned)(r0 * ow + ucol));
-              if (pair) {
-                *reinterpret_cast<float2*>(d0) = make_float2(o00, o01);
-              } else {
-                d0[0] = o00;
-                if (two) d0[1] = o01;
+            if (pair && r0 + 1 < oh) {  // the common case in one block (see the PK form)
+              *reinterpret_cast<float2*>(at32(dst, (unsigned)(r0 * ow + ucol))) = make_float2(o00, o01);
+              *reinterpret_cast<float2*>(at32(dst, (unsigned)((r0 + 1) * ow + ucol))) = make_float2(o10, o11);
+            } else {
+              if (r0 < oh) {
+                float* d0 = at32(dst, (unsigned)(r0 * ow + ucol));
+                if (pair) {
+                  *reinterpret_cast<float2*>(d0) = make_float2(o00, o01);
+                } else {
+                  d0[0] = o00;
+                  if (two) d0[1] = o01;
+                }
               }
-            }
-            if (r0 + 1 < oh) {
-              float* d1 = at32(dst, (unsigned)((r0 + 1) * ow + ucol));
-              if (pair) {
-                *reinterpret_cast<float2*>(d1) = make_float2(o10, o11);
-              } else {
-                d1[0] = o10;
-                if (two) d1[1] = o11;
+              if (r0 + 1 < oh) {
+                float* d1 = at32(dst, (unsigned)((r0 + 1) * ow + ucol));
+                if (pair) {
+                  *reinterpret_cast<float2*>(d1) = make_float2(o10, o11);
+                } else {
+                  d1[0] = o10;
+                  if (two) d1[1] = o11;
+                }
               }
             }
           }
