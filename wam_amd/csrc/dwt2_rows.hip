@@ -260,7 +260,11 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
   constexpr int p = L - 2;
   __shared__ __attribute__((aligned(16))) float rows[kWaves][C][kRowLds];
   const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR bases
+  // wave-uniform wave index (SGPR bases) except in the windowed form: there the uniform form's
+  // lower register count (165 vs 195 VGPRs: 3 instead of 2 waves per SIMD) let more strips of a
+  // 28-alpha launch compete for L2 -- PMC/algorithmic 1.05 -> 1.13 and the c4 level-0 launch
+  // 3,462 -> 3,633-3,894 us (profiles/r04x_ab_adj28.log) -- while levels 1-2 gain 15-17 %
+  const int wv = WIN ? (int)(threadIdx.x >> 6) : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t gw = wam_xcd_block(blockIdx.x, gridDim.x) * kWaves + wv;
   if (gw >= total_waves) return;
   // strip fastest: the strips of one (plane, row chunk) -- which fetch the same source rows --
