@@ -152,6 +152,10 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
       const uint32_t nw4 = (uint32_t)nw / 4u;
       wam_normal4_x2(rowg + (uint32_t)(sra >= 0 ? sra : 0) * nw4, rowg + (uint32_t)(srb >= 0 ? srb : 0) * nw4,
                      (uint32_t)(img + nz.image_base), (uint32_t)smp, nz.k0, nz.k1, za, zb);
+      // both blocks used here: otherwise the compiler sinks row b's chain to its consume() one row
+      // later and the two Philox chains no longer interleave
+      asm volatile("" ::"v"(za[0]), "v"(za[1]), "v"(za[2]), "v"(za[3]), "v"(zb[0]), "v"(zb[1]), "v"(zb[2]),
+                   "v"(zb[3]));
     }
   };
 
