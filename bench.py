@@ -19,8 +19,9 @@ network). One STEP = one explainer call on the config's whole batch:
   c3-c5 state no reduced model precision, so their credited value runs the model in fp32 (the
   reference's); the bf16 model is reported beside it as variants.bf16_model.
 Multi-GPU (one process per GPU, RCCL): the explainer itself shards ONE call of the batch with
-dist=True -- c2/c4 over the batch (each rank a contiguous image range, the per-sample
-batch-global maxima combined by an all-reduce MAX, the rows gathered), c3/c5 over the noise
+dist=True -- c2 over the batch (each rank a contiguous image range, the per-sample batch-global
+maxima combined by an all-reduce MAX, the rows gathered), c4 over the IG path steps as BASELINE
+configs[3] names it (trapezoid partials summed by one fp32 all-reduce), c3/c5 over the noise
 samples (partial accumulators summed by an all-reduce) -- so "scaling" is "strong" and value =
 the call's attributions / max-over-ranks time. N > 1 also reports the collectives' time and a
 weak-scaling figure (each rank its own batch, no collective) as secondary fields.
@@ -136,7 +137,7 @@ def workload(name):
                         dict(wavelet="sym8", J=5, method="integratedgrad", mode="reflect", n_samples=64,
                              frame="native"), "fp32",
                         "c4: WAM-2D sym8 J=5 Integrated Gradients (64 path steps), batch 128 x 512x512, ResNet-50",
-                        "images")
+                        "samples")  # BASELINE configs[3]: path steps sharded, one fp32 all-reduce SUM
     if name == "c5":
         return Workload("c5", 3, "WAM-3D attributions/sec @128^3 n_samples=25 (haar J=2 SmoothGrad, Voxel3D)",
                         "attributions/s", 16, 25, lambda: testmodels.voxel_volumes(16),
@@ -692,6 +693,8 @@ def collectives_timing(wl, dev, world, axis):
         rows = torch.zeros(hi - lo, H * H, dtype=torch.float64, device=dev)
         ops.append(("all_reduce_max_band_maxima", lambda: shard.all_reduce_max(t)))
         ops.append(("all_gather_frame_rows", lambda: shard.all_gather_rows(rows, wl.n)))
+        out_bytes = {"all_reduce_max_band_maxima_bytes": int(t.numel() * 4),
+                     "all_gather_frame_rows_bytes": int(-(-wl.n // world) * world * H * H * 8)}
     else:
         if wl.dim == 1:
             p = P.get_plan(1, (80000,), wl.kw["J"], wl.kw["wavelet"], wl.kw["mode"], dev)
@@ -699,11 +702,14 @@ def collectives_timing(wl, dev, world, axis):
             dt = torch.float32
         elif wl.dim == 3:
             numel, dt = wl.n * 128 ** 3, torch.float32
+        elif wl.name == "c4":  # IG: the fp32 trapezoid accumulator of the whole batch
+            numel, dt = wl.n * 512 * 512, torch.float32
         else:
             numel, dt = wl.n * 224 * 224, torch.float64
         acc = torch.zeros(numel, dtype=dt, device=dev)
         ops.append(("all_reduce_sum_accumulators", lambda: shard.all_reduce_sum(acc)))
-    out = {}
+        out_bytes = {"all_reduce_sum_accumulators_bytes": int(numel * acc.element_size())}
+    out = dict(out_bytes)
     for tag, fn in ops:
         fn()
         torch.cuda.synchronize(dev)

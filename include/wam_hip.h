@@ -53,11 +53,12 @@ int wam_plan_create(wam_plan** plan, int ndim, const int64_t* shape, int levels,
 /* flags: WAM_PLAN_GENERIC forces the per-axis kernels, WAM_PLAN_NO_ROWS skips the row-resident
  * and plane-resident 2D kernels, WAM_PLAN_NO_PLANE skips only the plane-resident (all levels in
  * one workgroup) kernels; WAM_PLAN_NO_COOP / WAM_PLAN_FORCE_COOP pick the plane kernels' level-1
- * form (wave chunks / cooperative row stream) instead of the size-based choice (all used by tests
+ * form (wave chunks / cooperative row stream) and WAM_PLAN_LINE selects the line-streaming SmoothGrad
+ * analysis (one wave per plane, all levels streamed) instead of the size-based choice (all used by tests
  * to cross-check the fused 2D kernels); 0 selects the fastest path.
  * wam_plan_create == wam_plan_create_ex(..., 0). */
 enum wam_plan_flags { WAM_PLAN_GENERIC = 1, WAM_PLAN_NO_ROWS = 2, WAM_PLAN_NO_PLANE = 4, WAM_PLAN_NO_COOP = 8,
-                      WAM_PLAN_FORCE_COOP = 16 };
+                      WAM_PLAN_FORCE_COOP = 16, WAM_PLAN_LINE = 32 };
 int wam_plan_create_ex(wam_plan** plan, int ndim, const int64_t* shape, int levels,
                        const double* dec_lo, const double* dec_hi,
                        const double* rec_lo, const double* rec_hi, int filt_len, int mode, int flags);
@@ -149,6 +150,13 @@ int wam_timing_drain(int max_records, char* names, float* ms, double* bytes);
 /* sigma[i] = fp32(spread) * (max(x_i[0:len]) - min(x_i[0:len])), x_i = x + i*item_stride */
 int wam_item_sigma(int64_t items, int64_t item_stride, int64_t len, const float* x, float spread,
                    float* sigma, void* stream);
+/* the same sigma as a full-chip split reduction (items x ranges workgroups; the last range of an
+ * item to finish combines the partials). ws: wam_item_sigma_ws_bytes(items, len) bytes, 8-byte
+ * aligned, zero-filled before its first use with these (items, len); the call leaves it reusable
+ * for the same (items, len). */
+int64_t wam_item_sigma_ws_bytes(int64_t items, int64_t len);
+int wam_item_sigma_ws(int64_t items, int64_t item_stride, int64_t len, const float* x, float spread,
+                      float* sigma, void* ws, int64_t ws_bytes, void* stream);
 
 /* out[s, i, e] = x[i, e] + noise  for e < noised_len,  0 for noised_len <= e < item_stride
  * noise = host_noise[s, i, e] if host_noise != NULL (parity mode: the numpy legacy stream), else

@@ -139,6 +139,15 @@ class TinySmooth2D(nn.Module):
         return self.fc(torch.flatten(h, 1))
 
 
+class TinySmooth2DAux(TinySmooth2D):
+    """TinySmooth2D with a trainable head that forward() never uses: loss.backward() leaves its
+    .grad None, and so must a sharded call (engine.param_grad_sum)."""
+
+    def __init__(self, c_in=3, n_classes=10, seed=7):
+        super().__init__(c_in, n_classes, seed)
+        self.aux = nn.Linear(4, 4)
+
+
 class TinyAudio(nn.Module):
     def __init__(self, n_classes=10, seed=11):
         super().__init__()

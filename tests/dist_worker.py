@@ -45,6 +45,9 @@ def cases():
            dict(wavelet="db4", J=2, n_samples=25, noise="philox", frame="native"))
     yield ("2d_ig_auto_uneven_23", "2D", m2, x23, y23,
            dict(wavelet="haar", J=2, method="integratedgrad", n_samples=25, frame="native"))
+    # a trainable head forward() never uses: .grad stays None on every rank
+    yield ("2d_smooth_unused_head_samples", "2D", testmodels.TinySmooth2DAux, x2, [1, 4, 2],
+           dict(wavelet="haar", J=2, n_samples=3, dist_axis="samples"))
     yield ("2d_smooth_numpy_samples", "2D", m2, x2, [1, 4, 2],
            dict(wavelet="haar", J=3, n_samples=5, dist_axis="samples"))
     yield ("2d_smooth_philox_images", "2D", m2, x2, [1, 4, 2],

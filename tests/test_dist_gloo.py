@@ -96,6 +96,14 @@ def _worker(rank, world, port, q):
                 if a1 > a0:
                     engine.input_gradient(pm, xg[2 * a0:2 * a1], [1, 2], a1 - a0, 2)
             res["pgrad%d" % n_smp] = [p_.grad.clone().numpy() for p_ in pm.parameters()]
+        # a trainable parameter no rank reaches (an unused head) keeps .grad None, as the
+        # single-process loss.backward() leaves it (not zeros: optimizers would step on zeros)
+        pa = testmodels.TinySmooth2DAux()
+        a0, a1 = shard.range(3)
+        with engine.param_grad_sum(engine.trainable_params(pa), shard):
+            engine.input_gradient(pa, xg[2 * a0:2 * a1], [1, 2], a1 - a0, 2)
+        res["aux_grad_none"] = pa.aux.weight.grad is None and pa.aux.bias.grad is None
+        res["aux_conv_grad"] = pa.conv.weight.grad.clone().numpy()
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -136,5 +144,9 @@ def test_two_rank_sharding_matches_single_process():
             engine.input_gradient(pm, xg[:2 * n_smp], [1, 2], n_smp, 2)
             for got, p_ in zip(out[r]["pgrad%d" % n_smp], pm.parameters()):
                 assert np.allclose(got, p_.grad.numpy(), rtol=1e-5, atol=1e-7)
+        assert out[r]["aux_grad_none"]
+        pa = testmodels.TinySmooth2DAux()
+        engine.input_gradient(pa, xg[:6], [1, 2], 3, 2)
+        assert np.allclose(out[r]["aux_conv_grad"], pa.conv.weight.grad.numpy(), rtol=1e-5, atol=1e-7)
         assert out[r]["smooth_images"].shape == ref3.shape
         assert np.abs(out[r]["smooth_images"] - ref3).max() < 1e-6

@@ -195,6 +195,19 @@ def test_wam_budget_override():
     assert engine.wam_budget_bytes() >= 1 << 30
 
 
+def test_wam_budget_tiers(monkeypatch):
+    """The default budget is rounded to a tier, so a call's split into passes does not drift with
+    the allocator; ranks sharing a device are not divided twice (free memory already counts them)."""
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert engine.budget_tier(36 << 30) == 36 << 30
+    assert engine.budget_tier((37 << 30) + 12345) == 36 << 30
+    assert engine.budget_tier(9 << 30) == 8 << 30
+    assert engine.budget_tier(3 << 30) == 2 << 30
+    assert engine.budget_tier(1 << 30) == 1 << 30
+    b = engine.wam_budget_bytes()
+    assert b == engine.budget_tier(b) and b >= 1 << 30
+
+
 def test_legacy_noise_stream_matches_reference_loop():
     x = torch.tensor(np.random.RandomState(3).standard_normal((3, 2, 5, 5)).astype(np.float32))
     sig = [float(0.25 * (x[i].max() - x[i].min())) for i in range(3)]

@@ -43,6 +43,8 @@ _SIGS = {
     "wam_waverec": (c_int, [c_vp, c_i64, c_vp, ctypes.POINTER(c_f32), c_int, c_vp, c_vp, c_vp]),
     "wam_waverec_adjoint": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "wam_item_sigma": (c_int, [c_i64, c_i64, c_i64, c_vp, c_f32, c_vp, c_vp]),
+    "wam_item_sigma_ws_bytes": (c_i64, [c_i64, c_i64]),
+    "wam_item_sigma_ws": (c_int, [c_i64, c_i64, c_i64, c_vp, c_f32, c_vp, c_vp, c_i64, c_vp]),
     "wam_noise_add": (c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, ctypes.c_uint64, c_i64, c_vp, c_vp]),
     "wam_noise_add_ex": (c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, ctypes.c_uint64, c_i64, c_i64, c_vp,
                                  c_vp]),

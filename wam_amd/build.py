@@ -1,18 +1,27 @@
 """Build libwam_hip.so (gfx950) in-tree with hipcc.
 
-    python -m wam_amd.build            # or: python wam_amd/build.py
+    python wam_amd/build.py            # or: python -m wam_amd.build
 
 No RPATH to /opt/rocm is recorded: the library binds to the libamdhip64.so.7 that torch has
 already loaded (import torch before loading it; see wam_amd/_lib.py).
+
+Objects are cached under build/obj/ by a hash of their source, the shared headers and the compile
+line, so a build after a one-file change (and the variant builds of scripts/build_variants.py)
+recompiles that file only.
 """
+import hashlib
 import os
+import shutil
 import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libwam_hip.so")
-SOURCES = ["plan.hip", "dwt_axis.hip", "dwt2_fused.hip", "dwt2_rows.hip", "dwt2_plane.hip", "dwt1_tile.hip", "dwt3_haar.hip", "epilogue.hip", "evaluate.hip", "visualize3d.hip", "melspec.hip", "model_ew.hip"]
+OBJ_CACHE = os.path.join(os.path.dirname(HERE), "build", "obj")
+SOURCES = ["plan.hip", "dwt_axis.hip", "dwt2_fused.hip", "dwt2_rows.hip", "dwt2_plane.hip", "dwt2_line.hip",
+           "dwt1_tile.hip", "dwt3_haar.hip", "epilogue.hip", "evaluate.hip", "visualize3d.hip", "melspec.hip",
+           "model_ew.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("WAM_OFFLOAD_ARCH", "gfx950")
 
@@ -26,34 +35,47 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _key(src, cmd):
+    h = hashlib.sha1(" ".join(cmd[:-3]).encode())
+    hdrs = sorted(f for f in os.listdir(CSRC) if f.endswith(".hpp"))
+    for f in [src] + [os.path.join(CSRC, x) for x in hdrs] + [os.path.join(CSRC, "..", "..", "include", "wam_hip.h")]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def build(force=False, verbose=False):
     if not force and not _stale():
         return OUT
+    os.makedirs(OBJ_CACHE, exist_ok=True)
     objs = []
     jobs = []
     for src in SOURCES:
-        obj = os.path.join(CSRC, src.replace(".hip", ".o"))
+        path = os.path.join(CSRC, src)
+        tmp_obj = os.path.join(CSRC, src.replace(".hip", ".o"))
         cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-c",
-               "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
-               os.path.join(CSRC, src), "-o", obj]
-        objs.append(obj)
-        jobs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+               "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics", path, "-o", tmp_obj]
+        cached = os.path.join(OBJ_CACHE, "%s.%s.o" % (src, _key(path, cmd)))
+        objs.append(cached)
+        if os.path.exists(cached):
+            continue
+        jobs.append((src, tmp_obj, cached, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     failed = False
-    for src, j in zip(SOURCES, jobs):
+    for src, tmp_obj, cached, j in jobs:
         out, _ = j.communicate()
         if verbose or j.returncode:
             sys.stderr.write(out.decode())
         if j.returncode:
             failed = True
             sys.stderr.write("hipcc failed on %s\n" % src)
+        else:
+            shutil.move(tmp_obj, cached)
     if failed:
         raise RuntimeError("libwam_hip.so build failed")
     tmp = OUT + ".tmp"
     link = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs
     subprocess.check_call(link)
     os.replace(tmp, OUT)
-    for o in objs:
-        os.remove(o)
     return OUT
 
 

@@ -212,7 +212,10 @@ int launch_syn_L(int64_t batch, const float* H, const float* V, const float* D, 
 }  // namespace
 
 bool dwt2_fused_supported(const wam_plan* p) {
-  return p->ndim == 2 && p->L <= 20 && !(p->L & 1) && (p->shape[0] < (1 << 30)) && (p->shape[1] < (1 << 30));
+  // the streaming synthesis addresses a plane with 32-bit byte offsets (rowtools.hpp at32): a plane
+  // of 2^30 floats or more would wrap, so such plans take the per-axis kernels
+  return p->ndim == 2 && p->L <= 20 && !(p->L & 1) && (p->shape[0] < (1 << 30)) && (p->shape[1] < (1 << 30)) &&
+         p->shape[0] * p->shape[1] < (int64_t(1) << 30) && p->rec_shape[0] * p->rec_shape[1] < (int64_t(1) << 30);
 }
 
 int launch_dwt2_analysis_fused(const wam_plan* p, int64_t batch, const float* in, const int64_t* in_dims,

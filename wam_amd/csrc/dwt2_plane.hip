@@ -836,6 +836,8 @@ int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in
   const double in_planes = nz ? (double)nz->images * nz->channels : (double)items;
   const double bytes = 4.0 * (in_planes * nh0 * nw0 + (double)items * p->band_off[p->nbands]);
   if (nz) {
+    const int rc = launch_dwt2_line_analysis(p, items, in, coeffs, nz, n_samples, st);
+    if (rc != WAM_ERR_UNSUPPORTED) return rc;
     if (items != n_samples * nz->images * nz->channels) return WAM_ERR_INVALID_ARG;
     // the fused noise counts element groups of an image in 32 bits (wam_normal4_x2)
     if ((int64_t)nz->channels * nh0 * nw0 >= (int64_t(1) << 34)) return WAM_ERR_UNSUPPORTED;
@@ -876,6 +878,7 @@ int syn_lds_floats(const wam_plan* p, int& lcap, int& scap) {
 
 bool syn_ok(const wam_plan* p) {
   if (p->ndim != 2 || !l_ok(p->L) || p->levels < 1 || p->levels > WAM_MAX_LEVELS) return false;
+  if (p->rec_shape[0] * p->rec_shape[1] >= (int64_t(1) << 30)) return false;  // 32-bit byte offsets (at32)
   const int outq = 65 - p->L / 2;
   for (int l = 0; l < p->levels; ++l) {
     const int64_t ow = l ? p->lout[l - 1][1] : p->rec_shape[1];

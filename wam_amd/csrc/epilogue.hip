@@ -72,6 +72,97 @@ __global__ void __launch_bounds__(1024) k_item_sigma(const float* __restrict__ x
   }
 }
 
+// Full-chip form (wam_item_sigma_ws): each item is split into `chunks` ranges, one 256-thread
+// workgroup per (item, range) -- thousands of workgroups where the one-block-per-item form had 16
+// (c5) to 256 (c3) -- and the last workgroup of an item to arrive (arrival counter in the caller's
+// workspace) combines the partial (max, min) pairs. max / min are exact, so the result is the
+// single-block kernel's bit for bit, NaN propagation included.
+constexpr int kSigT = 256;
+template <bool VEC4>
+__global__ void __launch_bounds__(kSigT) k_item_sigma_split(const float* __restrict__ x, int64_t item_stride,
+                                                            int64_t len, int64_t chunk, int chunks, float spread,
+                                                            float* __restrict__ sigma, float2* __restrict__ part,
+                                                            unsigned int* __restrict__ cnt) {
+  const int64_t wg = blockIdx.x, item = wg / chunks;
+  const int64_t b = (wg - item * chunks) * chunk, e = min(len, b + chunk);
+  const float* xi = x + item * item_stride;
+  float mx = -INFINITY, mn = INFINITY;
+  if constexpr (VEC4) {  // chunk and len multiples of 4
+    const float4* x4 = reinterpret_cast<const float4*>(xi);
+    const int64_t e4 = e >> 2;
+    int64_t i = (b >> 2) + threadIdx.x;
+    for (; i + 3 * kSigT < e4; i += 4 * kSigT) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = x4[i + u * kSigT];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        mx = nan_max(nan_max(mx, v[u].x), nan_max(nan_max(v[u].y, v[u].z), v[u].w));
+        mn = nan_min(nan_min(mn, v[u].x), nan_min(nan_min(v[u].y, v[u].z), v[u].w));
+      }
+    }
+    for (; i < e4; i += kSigT) {
+      const float4 v = x4[i];
+      mx = nan_max(nan_max(mx, v.x), nan_max(nan_max(v.y, v.z), v.w));
+      mn = nan_min(nan_min(mn, v.x), nan_min(nan_min(v.y, v.z), v.w));
+    }
+  } else {
+    for (int64_t i = b + threadIdx.x; i < e; i += kSigT) {
+      const float v = xi[i];
+      mx = nan_max(mx, v);
+      mn = nan_min(mn, v);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = nan_max(mx, __shfl_xor(mx, o, 64));
+    mn = nan_min(mn, __shfl_xor(mn, o, 64));
+  }
+  __shared__ float smx[kSigT / 64], smn[kSigT / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    smx[wv] = mx;
+    smn[wv] = mn;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  for (int w = 1; w < kSigT / 64; ++w) {
+    mx = nan_max(mx, smx[w]);
+    mn = nan_min(mn, smn[w]);
+  }
+  if (chunks == 1) {
+    sigma[item] = spread * (mx - mn);
+    return;
+  }
+  part[wg] = make_float2(mx, mn);
+  __threadfence();  // release: the partial is visible device-wide before the arrival counts
+  const unsigned int arrived = atomicAdd(cnt + item, 1u);
+  if (arrived != (unsigned)chunks - 1) return;
+  __threadfence();  // acquire: every other range's partial is visible
+  const unsigned long long* pp = reinterpret_cast<const unsigned long long*>(part + item * chunks);
+  float MX = -INFINITY, MN = INFINITY;
+  for (int k = 0; k < chunks; ++k) {
+    // agent-scope loads: served past this CU's L1, which may hold the workspace from an earlier call
+    const unsigned long long u = __hip_atomic_load(pp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    MX = nan_max(MX, __uint_as_float((unsigned)u));
+    MN = nan_min(MN, __uint_as_float((unsigned)(u >> 32)));
+  }
+  // torch: spread * (max - min) in fp32 with the python scalar cast to fp32
+  sigma[item] = spread * (MX - MN);
+  cnt[item] = 0u;  // the workspace is left zeroed for the next call
+}
+
+// ranges per item: ~2,048 workgroups over the call, >= 4,096 floats per range
+void sigma_split(int64_t items, int64_t len, bool vec4, int64_t& chunk, int& chunks) {
+  int64_t c = (2048 + items - 1) / items;
+  const int64_t cap = len / 4096 > 1 ? len / 4096 : 1;
+  if (c > cap) c = cap;
+  if (c < 1) c = 1;
+  chunk = (len + c - 1) / c;
+  if (vec4) chunk = (chunk + 3) & ~int64_t(3);
+  chunks = (int)((len + chunk - 1) / chunk);
+}
+
 // ------------------------------------------------------------------------------ Philox noise
 // One thread per group of 4 consecutive elements of an item: one Philox call -> 4 normals.
 // VEC4: item_stride % 4 == 0, so groups never straddle items and loads/stores are 16 B.
@@ -556,6 +647,41 @@ int wam_item_sigma(int64_t items, int64_t item_stride, int64_t len, const float*
   else
     hipLaunchKernelGGL(k_item_sigma<false>, dim3((unsigned)items), dim3(1024), 0, (hipStream_t)stream, x, item_stride,
                        len, spread, sigma);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int64_t wam_item_sigma_ws_bytes(int64_t items, int64_t len) {
+  if (items < 1 || len < 1) return 0;
+  int64_t chunk;
+  int chunks;
+  sigma_split(items, len, false, chunk, chunks);
+  return items * (int64_t)chunks * (int64_t)sizeof(float2) + items * (int64_t)sizeof(unsigned int) + 16;
+}
+
+int wam_item_sigma_ws(int64_t items, int64_t item_stride, int64_t len, const float* x, float spread, float* sigma,
+                      void* ws, int64_t ws_bytes, void* stream) {
+  if (items < 0 || len < 1 || !x || !sigma) return WAM_ERR_INVALID_ARG;
+  if (items == 0) return WAM_OK;
+  if (!ws || ws_bytes < wam_item_sigma_ws_bytes(items, len) || ((uintptr_t)ws & 7)) return WAM_ERR_INVALID_ARG;
+  const bool vec4 = item_stride % 4 == 0 && len % 4 == 0 && (uintptr_t)x % 16 == 0;
+  int64_t chunk;
+  int chunks;
+  sigma_split(items, len, false, chunk, chunks);  // the split the workspace was sized for
+  if (vec4) {
+    chunk = (chunk + 3) & ~int64_t(3);
+    chunks = (int)((len + chunk - 1) / chunk);  // <= the sized count
+  }
+  float2* part = reinterpret_cast<float2*>(ws);
+  unsigned int* cnt = reinterpret_cast<unsigned int*>(part + items * chunks);
+  WamTimer tm((hipStream_t)stream, "k_item_sigma", 4.0 * (double)items * len);
+  const dim3 grid((unsigned)(items * chunks));
+  if (vec4)
+    hipLaunchKernelGGL(k_item_sigma_split<true>, grid, dim3(kSigT), 0, (hipStream_t)stream, x, item_stride, len, chunk,
+                       chunks, spread, sigma, part, cnt);
+  else
+    hipLaunchKernelGGL(k_item_sigma_split<false>, grid, dim3(kSigT), 0, (hipStream_t)stream, x, item_stride, len,
+                       chunk, chunks, spread, sigma, part, cnt);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }

@@ -148,14 +148,21 @@ def param_grad_sum(params, shard):
         sink = _PARAM_SINK
     finally:
         _PARAM_SINK = prev
+    # one flat SUM: the increments, then one has-gradient flag per parameter. A parameter that no
+    # rank reached (an unused head, a branch not taken) keeps .grad untouched, as loss.backward()
+    # leaves it in the single-process call; zeros would make optimizers treat it as a gradient.
+    dev = params[0].device
+    flags = torch.tensor([1.0 if p in sink else 0.0 for p in params], dtype=torch.float32, device=dev)
     flat = torch.cat([(sink[p] if p in sink else torch.zeros(p.shape, dtype=torch.float32, device=p.device))
-                      .reshape(-1) for p in params])
+                      .reshape(-1).to(dev) for p in params] + [flags])
     shard.all_reduce_sum(flat)
+    got = flat[-len(params):].tolist()
     off = 0
-    for p in params:
+    for p, f in zip(params, got):
         gp = flat[off:off + p.numel()].view(p.shape)
         off += p.numel()
-        _accumulate_param_grad(p, gp)
+        if f > 0:
+            _accumulate_param_grad(p, gp)
 
 
 class GradModel:
@@ -400,7 +407,10 @@ def wam_budget_bytes(device=None):
     """Device memory the WAM buffers of one transform pass may take: an eighth of the device's HBM,
     8-64 GiB (36 GiB on a 288 GB MI355X), capped by half of what is free on the device now (free
     HBM plus this process's cached, unallocated blocks: the model's own footprint and other
-    processes are already out of it) and shared by the ranks of this node that use the same device.
+    processes -- ranks sharing the device included -- are already out of it), rounded down to a
+    tier (multiples of 4 GiB from 8 GiB up, powers of two below) so that the split of a call into
+    passes (and with it the fp32 summation order of the trapezoid / frame sums) does not follow the
+    caching allocator from call to call.
     Larger passes read the trapezoid accumulators and the synthesis details fewer times per call.
     BUDGET_BYTES overrides it."""
     if BUDGET_BYTES is not None:
@@ -412,13 +422,18 @@ def wam_budget_bytes(device=None):
             budget = min(max(total // 8, 8 << 30), 64 << 30)
             free, _ = torch.cuda.mem_get_info(device)
             free += torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
-            import os
-            local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
-            share = max(1, -(-local // max(1, torch.cuda.device_count())))
-            budget = min(budget, max(free // 2, 1 << 30) // share)
+            budget = min(budget, max(free // 2, 1 << 30))
     except (RuntimeError, AssertionError, ValueError):
         pass
-    return int(budget)
+    return budget_tier(budget)
+
+
+def budget_tier(b):
+    """Round a byte budget down to its tier: multiples of 4 GiB from 8 GiB, powers of two below."""
+    b = int(b)
+    if b >= 8 << 30:
+        return (b >> 32) << 32
+    return 1 << (max(b, 1).bit_length() - 1)
 
 
 def wam_group(model_group, total, bytes_per_sample, budget_bytes=None):

@@ -173,6 +173,7 @@ PLAN_NO_ROWS = 2
 PLAN_NO_PLANE = 4
 PLAN_NO_COOP = 8
 PLAN_FORCE_COOP = 16
+PLAN_LINE = 32
 CAP_NOISY_WAVEDEC = 1
 CAP_ADJOINT_MAPS = 2
 
@@ -197,11 +198,25 @@ def timing_drain():
 
 
 # -------------------------------------------------------------------- WAM epilogue wrappers
+# (device, items, len) -> zero-initialised workspace of the split sigma reduction (its arrival
+# counters are reset by every call, so one buffer serves every call of that shape)
+_SIGMA_WS = {}
+
+
 def item_sigma(x, item_stride, length, spread):
+    """sigma_i = fp32(spread) * (max - min) of item i (lib/wam_2D.py:396-399, lib/wam_1D.py:311-314,
+    lib/wam_3D.py:567-569), as a full-chip split reduction."""
     items = x.numel() // item_stride
     sigma = torch.empty(items, dtype=torch.float32, device=x.device)
-    check(lib.wam_item_sigma(items, item_stride, length, ptr(x), float(np.float32(spread)), ptr(sigma),
-                             stream_of(x.device)))
+    if items == 0:
+        return sigma
+    key = (str(x.device), int(items), int(length))
+    ws = _SIGMA_WS.get(key)
+    if ws is None:
+        nb = int(lib.wam_item_sigma_ws_bytes(items, length))
+        ws = _SIGMA_WS[key] = torch.zeros((nb + 7) // 8, dtype=torch.float64, device=x.device)
+    check(lib.wam_item_sigma_ws(items, item_stride, length, ptr(x), float(np.float32(spread)), ptr(sigma), ptr(ws),
+                                ws.numel() * 8, stream_of(x.device)))
     return sigma
 
 

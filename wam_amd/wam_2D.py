@@ -478,7 +478,9 @@ class WaveletAttribution2D(BaseWAM2D):
             coeff = z * float(np.float32(alpha))  # the path coefficients alpha * z of the last step
             self.wam._record_pass(plan_, coeff, None, n * c, 0, n, c, grad_img=last_g)
         if axis == "images":
-            base = shard.all_gather_rows(base.view(n, rh * rw), N)
+            # base holds ONE normalised fp32 map per pixel added to 0.0 in fp64 (frame_accumulate of
+            # a single sample), so its fp32 copy is exact: the gather moves half the bytes
+            base = shard.all_gather_rows(base.view(n, rh * rw).float(), N).double()
             acc = shard.all_gather_rows(acc.view(n, rh * rw), N)
         else:
             shard.all_reduce_sum(acc)
