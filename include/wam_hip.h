@@ -62,6 +62,12 @@ enum wam_plan_flags { WAM_PLAN_GENERIC = 1, WAM_PLAN_NO_ROWS = 2, WAM_PLAN_NO_PL
 int wam_plan_create_ex(wam_plan** plan, int ndim, const int64_t* shape, int levels,
                        const double* dec_lo, const double* dec_hi,
                        const double* rec_lo, const double* rec_hi, int filt_len, int mode, int flags);
+/* a host-only plan: the same geometry, band layout, caps and workspace queries, no device (no
+ * filters uploaded). Every compute entry point refuses it with WAM_ERR_INVALID_ARG. Used by the
+ * sanitizer build of the host code (tests/native/). */
+int wam_plan_create_host(wam_plan** plan, int ndim, const int64_t* shape, int levels,
+                         const double* dec_lo, const double* dec_hi,
+                         const double* rec_lo, const double* rec_hi, int filt_len, int mode, int flags);
 void wam_plan_destroy(wam_plan* plan);
 int wam_plan_num_bands(const wam_plan* plan);
 /* dims of band b (ndim values) */

@@ -69,6 +69,18 @@ def test_melspec_filters_and_spectrogram(W):
     assert spec.shape == (2, 513, 8000 // 256 + 1)
 
 
+def _record_gap(rec):
+    """The compute_spectrogram magnitude gap to librosa's iterate (parity unpinned: librosa absent),
+    appended as one JSON line to $WAM_TEST_RECORD_DIR (default gpurun_out/, merged back from the GPU
+    box) so that the size of the divergence is on record (profiles/r05_compute_spectrogram_gap.jsonl)."""
+    import json
+    import os
+    d = os.environ.get("WAM_TEST_RECORD_DIR", os.path.join(os.path.dirname(os.path.dirname(__file__)), "gpurun_out"))
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "compute_spectrogram_gap.jsonl"), "a") as f:
+        f.write(json.dumps(rec) + "\n")
+
+
 def _nnls_obj(A, x, B):
     return 0.5 * float(np.sum((A.astype(np.float64) @ x.astype(np.float64) - B) ** 2))
 
@@ -103,9 +115,14 @@ def test_compute_spectrogram_nnls(W, sr, n_fft, n_mels, T):
         # the returned magnitudes themselves: a different point of the NNLS solution set than
         # librosa's early-stopped L-BFGS-B iterate (reported, not bounded: ADVICE r03)
         gap = np.abs(spec[i] - ref).max() / max(1e-30, np.abs(ref).max())
+        gap_l2 = float(np.linalg.norm(spec[i] - ref) / max(1e-30, np.linalg.norm(ref)))
         rgap = np.abs(A @ (ref.astype(np.float64) ** 2) - A @ xe).max() / np.abs(B).max()
-        print("compute_spectrogram vs librosa-restated L-BFGS-B: max |x gap| %.3e of max |x|, "
-              "re-projection gaps: device %.2e, L-BFGS-B %.2e of max |B|" % (gap, err, rgap))
+        _record_gap({"sr": sr, "n_fft": n_fft, "n_mels": n_mels, "frames": T, "waveform": i,
+                     "magnitude_gap_max_over_max": float(gap), "magnitude_gap_rel_l2": gap_l2,
+                     "reprojection_gap_device_over_max_B": float(err),
+                     "reprojection_gap_lbfgsb_over_max_B": float(rgap),
+                     "objective_device": fo, "objective_lbfgsb": _nnls_obj(A, ref.astype(np.float64) ** 2, B),
+                     "objective_exact_nnls": fe})
     # process_in_chunks (module function, lib/wam_1D.py:442-448): the same per-frame inversion in
     # chunks of 5 frames. The minimiser is not unique (more bins than bands) and the solver stops on
     # the worst column of a chunk, so chunkings agree on the re-projection A x (unique), not on x

@@ -33,6 +33,8 @@ _SIGS = {
     "wam_plan_create_ex": (c_int, [ctypes.POINTER(c_vp), c_int, c_i64p, c_int, c_dp, c_dp, c_dp, c_dp, c_int, c_int,
                                    c_int]),
     "wam_plan_destroy": (None, [c_vp]),
+    "wam_plan_create_host": (c_int, [ctypes.POINTER(c_vp), c_int, c_i64p, c_int, c_dp, c_dp, c_dp, c_dp, c_int,
+                                     c_int, c_int]),
     "wam_plan_num_bands": (c_int, [c_vp]),
     "wam_plan_band_shape": (c_int, [c_vp, c_int, c_i64p]),
     "wam_plan_band_offset": (c_i64, [c_vp, c_int]),

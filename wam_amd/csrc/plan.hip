@@ -38,24 +38,29 @@ int wam_plan_create(wam_plan** out, int ndim, const int64_t* shape, int levels, 
   return wam_plan_create_ex(out, ndim, shape, levels, dec_lo, dec_hi, rec_lo, rec_hi, L, mode, 0);
 }
 
-int wam_plan_create_ex(wam_plan** out, int ndim, const int64_t* shape, int levels, const double* dec_lo,
-                       const double* dec_hi, const double* rec_lo, const double* rec_hi, int L, int mode,
-                       int flags) {
-  if (!out || !shape || !dec_lo || !dec_hi || !rec_lo || !rec_hi) return WAM_ERR_INVALID_ARG;
+// geometry of a plan (sizes per level, crop flags, band layout, fp32 filters): host arithmetic only
+static int plan_geometry(wam_plan* p, int ndim, const int64_t* shape, int levels, const double* dec_lo,
+                         const double* dec_hi, const double* rec_lo, const double* rec_hi, int L, int mode,
+                         int flags) {
+  if (!shape || !dec_lo || !dec_hi || !rec_lo || !rec_hi) return WAM_ERR_INVALID_ARG;
   if (ndim < 1 || ndim > WAM_MAX_NDIM || levels < 1 || levels > WAM_MAX_LEVELS) return WAM_ERR_INVALID_ARG;
   if (L < 2 || L > WAM_MAX_FILT || (L & 1)) return WAM_ERR_UNSUPPORTED;
   if (mode < WAM_MODE_ZERO || mode > WAM_MODE_PERIODIC) return WAM_ERR_INVALID_ARG;
-  wam_plan* p = (wam_plan*)calloc(1, sizeof(wam_plan));
-  if (!p) return WAM_ERR_NO_MEMORY;
   p->ndim = ndim;
   p->levels = levels;
   p->L = L;
   p->mode = mode;
   p->flags = flags;
   p->pad = (2 * L - 3) / 2;
+  p->device = -1;
+  // each axis below 2^31 and the whole item below 2^40 elements: every per-item size and offset
+  // (and batch x offset products of sane batches) stays far from int64 overflow
+  int64_t vol = 1;
   for (int a = 0; a < ndim; ++a) {
-    if (shape[a] < 1) { free(p); return WAM_ERR_SHAPE; }
+    if (shape[a] < 1 || shape[a] >= (int64_t(1) << 31)) return WAM_ERR_SHAPE;
     p->shape[a] = shape[a];
+    if (shape[a] > ((int64_t(1) << 40) - 1) / vol) return WAM_ERR_SHAPE;  // vol * shape[a] >= 2^40
+    vol *= shape[a];
   }
   // analysis sizes per level
   for (int a = 0; a < ndim; ++a) {
@@ -63,7 +68,7 @@ int wam_plan_create_ex(wam_plan** out, int ndim, const int64_t* shape, int level
     for (int l = 0; l < levels; ++l) {
       p->lin[l][a] = n;
       int64_t m = (n + 2 * p->pad + (n % 2) - L) / 2 + 1;
-      if (m < 1) { free(p); return WAM_ERR_SHAPE; }
+      if (m < 1) return WAM_ERR_SHAPE;
       p->lout[l][a] = m;
       n = m;
     }
@@ -77,7 +82,7 @@ int wam_plan_create_ex(wam_plan** out, int ndim, const int64_t* shape, int level
       if (l > 0) {
         int64_t next = p->lout[l - 1][a];
         if (next == pred - 1) e = 1;
-        else if (next != pred) { free(p); return WAM_ERR_SHAPE; }
+        else if (next != pred) return WAM_ERR_SHAPE;
       } else {
         p->rec_shape[a] = pred;
       }
@@ -104,6 +109,20 @@ int wam_plan_create_ex(wam_plan** out, int ndim, const int64_t* shape, int level
     p->h_filt[WAM_F_ADJ_LO][k] = (float)rec_lo[k];
     p->h_filt[WAM_F_ADJ_HI][k] = (float)rec_hi[k];
   }
+  return WAM_OK;
+}
+
+int wam_plan_create_ex(wam_plan** out, int ndim, const int64_t* shape, int levels, const double* dec_lo,
+                       const double* dec_hi, const double* rec_lo, const double* rec_hi, int L, int mode,
+                       int flags) {
+  if (!out) return WAM_ERR_INVALID_ARG;
+  wam_plan* p = (wam_plan*)calloc(1, sizeof(wam_plan));
+  if (!p) return WAM_ERR_NO_MEMORY;
+  int rc = plan_geometry(p, ndim, shape, levels, dec_lo, dec_hi, rec_lo, rec_hi, L, mode, flags);
+  if (rc) {
+    free(p);
+    return rc;
+  }
   hipError_t e = hipGetDevice(&p->device);
   if (e != hipSuccess) { free(p); return WAM_ERR_HIP_BASE + (int)e; }
   e = hipMalloc((void**)&p->d_filt, sizeof(float) * WAM_F_COUNT * L);
@@ -113,6 +132,21 @@ int wam_plan_create_ex(wam_plan** out, int ndim, const int64_t* shape, int level
     for (int k = 0; k < L; ++k) packed[f * L + k] = p->h_filt[f][k];
   e = hipMemcpy(p->d_filt, packed.data(), sizeof(float) * packed.size(), hipMemcpyHostToDevice);
   if (e != hipSuccess) { (void)hipFree(p->d_filt); free(p); return WAM_ERR_HIP_BASE + (int)e; }
+  *out = p;
+  return WAM_OK;
+}
+
+int wam_plan_create_host(wam_plan** out, int ndim, const int64_t* shape, int levels, const double* dec_lo,
+                         const double* dec_hi, const double* rec_lo, const double* rec_hi, int L, int mode,
+                         int flags) {
+  if (!out) return WAM_ERR_INVALID_ARG;
+  wam_plan* p = (wam_plan*)calloc(1, sizeof(wam_plan));
+  if (!p) return WAM_ERR_NO_MEMORY;
+  int rc = plan_geometry(p, ndim, shape, levels, dec_lo, dec_hi, rec_lo, rec_hi, L, mode, flags);
+  if (rc) {
+    free(p);
+    return rc;
+  }
   *out = p;
   return WAM_OK;
 }
@@ -412,14 +446,14 @@ int analysis_driver(const wam_plan* p, int64_t batch, const float* x, float* coe
 extern "C" {
 
 int wam_wavedec(const wam_plan* p, int64_t batch, const float* x, float* coeffs, void* ws, void* stream) {
-  if (!p || !x || !coeffs || !ws || batch < 0) return WAM_ERR_INVALID_ARG;
+  if (!p || !p->d_filt || !x || !coeffs || !ws || batch < 0) return WAM_ERR_INVALID_ARG;
   if (batch == 0) return WAM_OK;
   return analysis_driver(p, batch, x, coeffs, ws, (hipStream_t)stream, false);
 }
 
 int wam_waverec_adjoint(const wam_plan* p, int64_t batch, const float* grad, float* coeff_grads, void* ws,
                         void* stream) {
-  if (!p || !grad || !coeff_grads || !ws || batch < 0) return WAM_ERR_INVALID_ARG;
+  if (!p || !p->d_filt || !grad || !coeff_grads || !ws || batch < 0) return WAM_ERR_INVALID_ARG;
   if (batch == 0) return WAM_OK;
   return analysis_driver(p, batch, grad, coeff_grads, ws, (hipStream_t)stream, true);
 }
@@ -441,7 +475,7 @@ int wam_plan_caps(const wam_plan* p) {
 int wam_wavedec_noisy_ex(const wam_plan* p, int64_t n_samples, int64_t images, int channels, const float* x,
                          const float* sigma, uint64_t seed, int64_t sample_base, int64_t image_base, float* coeffs,
                          void* ws, void* stream) {
-  if (!p || !x || !sigma || !coeffs || !ws || n_samples < 0 || images < 0 || channels < 1 || image_base < 0)
+  if (!p || !p->d_filt || !x || !sigma || !coeffs || !ws || n_samples < 0 || images < 0 || channels < 1 || image_base < 0)
     return WAM_ERR_INVALID_ARG;
   if (!(wam_plan_caps(p) & WAM_CAP_NOISY_WAVEDEC)) return WAM_ERR_UNSUPPORTED;
   const int64_t batch = n_samples * images * channels;
@@ -457,7 +491,7 @@ int wam_wavedec_noisy(const wam_plan* p, int64_t n_samples, int64_t images, int 
 
 int wam_waverec_adjoint_maps(const wam_plan* p, int64_t groups, int64_t group_items, int channels, const float* grad,
                              float* maps, float* band_max, float* coeff_grads, void* ws, void* stream) {
-  if (!p || !grad || !maps || !band_max || !ws || groups < 0 || group_items < 0 || channels < 1)
+  if (!p || !p->d_filt || !grad || !maps || !band_max || !ws || groups < 0 || group_items < 0 || channels < 1)
     return WAM_ERR_INVALID_ARG;
   if (!(wam_plan_caps(p) & WAM_CAP_ADJOINT_MAPS) || (channels != 1 && channels != 3)) return WAM_ERR_UNSUPPORTED;
   const int64_t images = groups * group_items;
@@ -495,7 +529,7 @@ int wam_waverec_adjoint_maps(const wam_plan* p, int64_t groups, int64_t group_it
 
 int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha, int n_alpha, float* out,
                 void* ws, void* stream) {
-  if (!p || !coeffs || !out || !ws || batch < 0 || n_alpha < 1) return WAM_ERR_INVALID_ARG;
+  if (!p || !p->d_filt || !coeffs || !out || !ws || batch < 0 || n_alpha < 1) return WAM_ERR_INVALID_ARG;
   if (!alpha && n_alpha != 1) return WAM_ERR_INVALID_ARG;
   if (batch == 0) return WAM_OK;
   hipStream_t st = (hipStream_t)stream;

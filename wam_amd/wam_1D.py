@@ -14,6 +14,7 @@ import torch
 from .engine import (Shard, auto_group, chunks, ig_weights, input_gradient, LegacyNoise, model_device,
                      param_grad_sum, require_gpu_device, trainable_params)
 from .melspec import kernel_supported, mel_adjoint, mel_forward, melspec_db
+from .profiling import phase
 from .plan import CAP_NOISY_WAVEDEC, accumulate_f32, get_plan, item_sigma, noise_add, trapz_stream
 
 
@@ -213,13 +214,16 @@ class WaveletAttribution1D(BaseWAM1D):
         c_acc = torch.zeros(n * plan.coeff_numel, dtype=torch.float32, device=dev)
         with param_grad_sum(trainable_params(self.model), shard):
             for s0, cnt in chunks(s_lo, s_hi, group):
-                if legacy is None and plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
-                    flat = plan.wavedec_noisy(x, sigma, cnt, n, 1, self.random_seed, s0)
-                else:
-                    host = None if legacy is None else legacy.chunk(s0, cnt)
-                    noisy = noise_add(x, sigma, cnt, n, w, w, seed=self.random_seed, sample_base=s0, host_noise=host)
-                    flat = plan.wavedec(noisy.view(cnt * n, w))
-                g_mel, cg = self._grads(plan, flat, cnt * n, y, cnt, n)
+                with phase("noise+wavedec"):
+                    if legacy is None and plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
+                        flat = plan.wavedec_noisy(x, sigma, cnt, n, 1, self.random_seed, s0)
+                    else:
+                        host = None if legacy is None else legacy.chunk(s0, cnt)
+                        noisy = noise_add(x, sigma, cnt, n, w, w, seed=self.random_seed, sample_base=s0,
+                                          host_noise=host)
+                        flat = plan.wavedec(noisy.view(cnt * n, w))
+                with phase("waverec+mel+model+adjoint"):
+                    g_mel, cg = self._grads(plan, flat, cnt * n, y, cnt, n)
                 if g_mel.numel() != cnt * mel_acc.numel():
                     raise RuntimeError("melspec gradient shape %s does not match %s" % (tuple(g_mel.shape),
                                                                                          self._mel_shape))
@@ -231,8 +235,9 @@ class WaveletAttribution1D(BaseWAM1D):
                 self.wam._record(plan, flat, cnt * n, (cnt - 1) * n, cg, cnt * n, (cnt - 1) * n, n)
         if legacy is not None:
             legacy.finish()
-        shard.all_reduce_sum(mel_acc)
-        shard.all_reduce_sum(c_acc)
+        with phase("collectives"):
+            shard.all_reduce_sum(mel_acc)
+            shard.all_reduce_sum(c_acc)
         accumulate_f32(mel_acc, 0, mel_acc, scale=float(self.n_samples))
         accumulate_f32(c_acc, 0, c_acc, scale=float(self.n_samples))
         mel = mel_acc.view(self._mel_shape).cpu().numpy().squeeze()

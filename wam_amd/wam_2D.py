@@ -31,6 +31,7 @@ import torch
 import torch.nn.functional as F
 
 from . import frames
+from .profiling import phase
 from .constants import WaveletDetailTuple2d
 from .engine import (GradModel, LegacyNoise, Shard, auto_group, chunks, ig_weights, model_device, param_grad_sum,
                      require_gpu_device, wam_budget_bytes, wam_group)
@@ -407,30 +408,39 @@ class WaveletAttribution2D(BaseWAM2D):
         last = None
         with param_grad_sum(self._grad.params(), shard):  # .grad as one process leaves it
             for s0, cnt in chunks(s_lo, s_hi, wgroup):
-                if legacy is not None:
-                    noisy = noise_add(xs, sigma, cnt, n, item, item, host_noise=legacy.chunk(s0, cnt, i_lo, i_hi))
-                    flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
-                elif plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
-                    flat = plan.wavedec_noisy(xs, sigma, cnt, n, c, self.random_seed, s0, image_base=i_lo)
-                else:
-                    noisy = noise_add(xs, sigma, cnt, n, item, item, seed=self.random_seed, sample_base=s0, item_base=i_lo)
-                    flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
-                img = plan.waverec(flat, cnt * n * c)[0].view((cnt * n, c) + rec)
-                g = self._gradients(img, y, cnt, n, group, batch)
-                maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
+                with phase("noise+wavedec2"):
+                    if legacy is not None:
+                        noisy = noise_add(xs, sigma, cnt, n, item, item, host_noise=legacy.chunk(s0, cnt, i_lo, i_hi))
+                        flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
+                    elif plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
+                        flat = plan.wavedec_noisy(xs, sigma, cnt, n, c, self.random_seed, s0, image_base=i_lo)
+                    else:
+                        noisy = noise_add(xs, sigma, cnt, n, item, item, seed=self.random_seed, sample_base=s0,
+                                          item_base=i_lo)
+                        flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
+                with phase("waverec2"):
+                    img = plan.waverec(flat, cnt * n * c)[0].view((cnt * n, c) + rec)
+                with phase("model"):
+                    g = self._gradients(img, y, cnt, n, group, batch)
+                with phase("adjoint+maps"):
+                    maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
                 if axis == "images":
-                    shard.all_reduce_max(bmax)  # per-sample maxima over the whole batch (A.6)
-                frame_accumulate(cnt, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, frame)
+                    with phase("all_reduce_max"):
+                        shard.all_reduce_max(bmax)  # per-sample maxima over the whole batch (A.6)
+                with phase("accumulate"):
+                    frame_accumulate(cnt, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs,
+                                     frame)
                 last = (plan, flat, None, cnt * n * c, (cnt - 1) * n, n, c)
                 last_g = g[(cnt - 1) * n:].reshape((n * c,) + rec)
         if legacy is not None:
             legacy.finish()
         if last is not None:
             self.wam._record_pass(*last, grad_img=last_g)
-        if axis == "images":
-            frame = shard.all_gather_rows(frame.view(n, rh * rw), N).reshape(-1)
-        else:
-            shard.all_reduce_sum(frame)
+        with phase("collectives"):
+            if axis == "images":
+                frame = shard.all_gather_rows(frame.view(n, rh * rw), N).reshape(-1)
+            else:
+                shard.all_reduce_sum(frame)
         avg = frame.view(N, rh, rw) / self.n_samples
         self._set_result(avg)
         return avg.cpu().numpy()
@@ -461,29 +471,35 @@ class WaveletAttribution2D(BaseWAM2D):
         last = None
         with param_grad_sum(self._grad.params(), shard):
             for k0, cnt in chunks(k_lo, k_hi, wgroup):
-                img = plan.waverec(z, n * c, alphas=alphas[k0:k0 + cnt]).view((cnt * n, c) + rec)
-                g = self._gradients(img, y, cnt, n, group, batch)
-                maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
+                with phase("waverec2(alpha)"):
+                    img = plan.waverec(z, n * c, alphas=alphas[k0:k0 + cnt]).view((cnt * n, c) + rec)
+                with phase("model"):
+                    g = self._gradients(img, y, cnt, n, group, batch)
+                with phase("adjoint+maps"):
+                    maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
                 if axis == "images":
-                    shard.all_reduce_max(bmax)
+                    with phase("all_reduce_max"):
+                        shard.all_reduce_max(bmax)
                 weights = None
                 if axis == "samples" and shard.world > 1:
                     weights = torch.from_numpy(ig_weights(k0, cnt, self.n_samples)).to(dev)
-                frame_trapz(cnt, k0, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs, prev, acc,
-                            weights)
+                with phase("trapz"):
+                    frame_trapz(cnt, k0, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs,
+                                prev, acc, weights)
                 last = (plan, float(alphas[k0 + cnt - 1]))
                 last_g = g[(cnt - 1) * n:].reshape((n * c,) + rec)
         if last is not None:
             plan_, alpha = last
             coeff = z * float(np.float32(alpha))  # the path coefficients alpha * z of the last step
             self.wam._record_pass(plan_, coeff, None, n * c, 0, n, c, grad_img=last_g)
-        if axis == "images":
-            # base holds ONE normalised fp32 map per pixel added to 0.0 in fp64 (frame_accumulate of
-            # a single sample), so its fp32 copy is exact: the gather moves half the bytes
-            base = shard.all_gather_rows(base.view(n, rh * rw).float(), N).double()
-            acc = shard.all_gather_rows(acc.view(n, rh * rw), N)
-        else:
-            shard.all_reduce_sum(acc)
+        with phase("collectives"):
+            if axis == "images":
+                # base holds ONE normalised fp32 map per pixel added to 0.0 in fp64 (frame_accumulate of
+                # a single sample), so its fp32 copy is exact: the gather moves half the bytes
+                base = shard.all_gather_rows(base.view(n, rh * rw).float(), N).double()
+                acc = shard.all_gather_rows(acc.view(n, rh * rw), N)
+            else:
+                shard.all_reduce_sum(acc)
         out = base.view(N, rh, rw) * acc.view(N, rh, rw).double()
         self._set_result(out)
         return out.cpu().numpy()

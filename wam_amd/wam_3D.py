@@ -22,6 +22,7 @@ from .constants import KEYS3
 from .engine import (LegacyNoise, Shard, auto_group, chunks, ig_weights, input_gradient, legacy3d_weights,
                      model_device, param_grad_sum, require_gpu_device, trainable_params)
 from ._lib import check, lib, ptr, stream_of
+from .profiling import phase
 from .plan import CAP_NOISY_WAVEDEC, cube_accumulate, get_plan, item_sigma, noise_add, subband_maps
 
 
@@ -292,13 +293,15 @@ class WaveletAttribution3D(BaseWAM3D):
                         full = torch.zeros((cnt, n, c) + sp, dtype=torch.float32, device=dev)
                         full[:, :, 0] = host
                         host = full
-                if host is None and c == 1 and plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
-                    flat = plan.wavedec_noisy(x, sigma, cnt, n, 1, self.random_seed, s0)
-                else:
-                    noisy = noise_add(x, sigma, cnt, n, c * vol, vol, seed=self.random_seed, sample_base=s0,
-                                      host_noise=host)
-                    flat = plan.wavedec(noisy.view((cnt * n * c,) + sp))
-                cg = self._grads(plan, flat, cnt * n * c, y, cnt, n, c)
+                with phase("noise+wavedec3"):
+                    if host is None and c == 1 and plan.caps & CAP_NOISY_WAVEDEC:  # noise fused on the load
+                        flat = plan.wavedec_noisy(x, sigma, cnt, n, 1, self.random_seed, s0)
+                    else:
+                        noisy = noise_add(x, sigma, cnt, n, c * vol, vol, seed=self.random_seed, sample_base=s0,
+                                          host_noise=host)
+                        flat = plan.wavedec(noisy.view((cnt * n * c,) + sp))
+                with phase("waverec3+model+adjoint"):
+                    cg = self._grads(plan, flat, cnt * n * c, y, cnt, n, c)
                 if shard.world == 1:
                     self._cube_from_grads(plan, cg, cnt * n * c, cnt, n, S, acc, 0, n_total=float(ns))
                 else:
@@ -308,7 +311,8 @@ class WaveletAttribution3D(BaseWAM3D):
                 self.wam._coeffs = None
         if legacy is not None:
             legacy.finish()
-        shard.all_reduce_sum(acc)
+        with phase("collectives"):
+            shard.all_reduce_sum(acc)
         self._cube_dev = acc.view(n, S, S, S)
         out = self._cube_dev.cpu().numpy()
         self.grads = out
