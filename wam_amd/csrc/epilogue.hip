@@ -91,12 +91,12 @@ __global__ void __launch_bounds__(kSigT) k_item_sigma_split(const float* __restr
     const float4* x4 = reinterpret_cast<const float4*>(xi);
     const int64_t e4 = e >> 2;
     int64_t i = (b >> 2) + threadIdx.x;
-    for (; i + 3 * kSigT < e4; i += 4 * kSigT) {
-      float4 v[4];
+    for (; i + 7 * kSigT < e4; i += 8 * kSigT) {  // 8 16-byte loads in flight per lane
+      float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = x4[i + u * kSigT];
+      for (int u = 0; u < 8; ++u) v[u] = x4[i + u * kSigT];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         mx = nan_max(nan_max(mx, v[u].x), nan_max(nan_max(v[u].y, v[u].z), v[u].w));
         mn = nan_min(nan_min(mn, v[u].x), nan_min(nan_min(v[u].y, v[u].z), v[u].w));
       }
@@ -119,42 +119,65 @@ __global__ void __launch_bounds__(kSigT) k_item_sigma_split(const float* __restr
     mn = nan_min(mn, __shfl_xor(mn, o, 64));
   }
   __shared__ float smx[kSigT / 64], smn[kSigT / 64];
+  __shared__ unsigned int last;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (lane == 0) {
     smx[wv] = mx;
     smn[wv] = mn;
   }
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  for (int w = 1; w < kSigT / 64; ++w) {
-    mx = nan_max(mx, smx[w]);
-    mn = nan_min(mn, smn[w]);
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kSigT / 64; ++w) {
+      mx = nan_max(mx, smx[w]);
+      mn = nan_min(mn, smn[w]);
+    }
+    if (chunks == 1) {
+      sigma[item] = spread * (mx - mn);
+      last = 0u;
+    } else {
+      // hand-off without fences (an agent-scope release writes back the whole L2 of this XCD --
+      // every dirty line the previous kernels left -- and cost more than the reduction): the
+      // partial goes out write-through (agent-scope store, sc1) and is drained before the arrival
+      // is counted (MI355X_MICROARCH.md, inter-workgroup visibility, the sc1 form)
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(part + wg),
+                         (unsigned long long)__float_as_uint(mx) | ((unsigned long long)__float_as_uint(mn) << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      last = __hip_atomic_fetch_add(cnt + item, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             (unsigned)chunks - 1;
+    }
   }
-  if (chunks == 1) {
-    sigma[item] = spread * (mx - mn);
-    return;
-  }
-  part[wg] = make_float2(mx, mn);
-  __threadfence();  // release: the partial is visible device-wide before the arrival counts
-  const unsigned int arrived = atomicAdd(cnt + item, 1u);
-  if (arrived != (unsigned)chunks - 1) return;
-  __threadfence();  // acquire: every other range's partial is visible
+  __syncthreads();
+  if (!last || wv != 0) return;
+  // the last range of the item: its first wave reads the partials with agent-scope (sc1) loads, one
+  // per lane, and reduces them across the wave
   const unsigned long long* pp = reinterpret_cast<const unsigned long long*>(part + item * chunks);
   float MX = -INFINITY, MN = INFINITY;
-  for (int k = 0; k < chunks; ++k) {
-    // agent-scope loads: served past this CU's L1, which may hold the workspace from an earlier call
+  for (int k = lane; k < chunks; k += 64) {
     const unsigned long long u = __hip_atomic_load(pp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     MX = nan_max(MX, __uint_as_float((unsigned)u));
     MN = nan_min(MN, __uint_as_float((unsigned)(u >> 32)));
   }
-  // torch: spread * (max - min) in fp32 with the python scalar cast to fp32
-  sigma[item] = spread * (MX - MN);
-  cnt[item] = 0u;  // the workspace is left zeroed for the next call
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    MX = nan_max(MX, __shfl_xor(MX, o, 64));
+    MN = nan_min(MN, __shfl_xor(MN, o, 64));
+  }
+  if (lane == 0) {
+    // torch: spread * (max - min) in fp32 with the python scalar cast to fp32
+    sigma[item] = spread * (MX - MN);
+    // the counter is left zeroed for the next call (write-through, like the partials)
+    __hip_atomic_store(cnt + item, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
-// ranges per item: ~2,048 workgroups over the call, >= 4,096 floats per range
+// ranges per item: >= 32 K floats per range (the arrivals on an item's counter are serialised at
+// the memory side: short ranges of many workgroups queue there -- c2 with 32 ranges of 4.7 K
+// floats per image ran 21 us), but at least ~512 workgroups over the call and >= 4 K floats each
 void sigma_split(int64_t items, int64_t len, bool vec4, int64_t& chunk, int& chunks) {
-  int64_t c = (2048 + items - 1) / items;
+  int64_t c = (len + 32767) / 32768;
+  const int64_t fill = (512 + items - 1) / items;
+  if (c < fill) c = fill;
   const int64_t cap = len / 4096 > 1 ? len / 4096 : 1;
   if (c > cap) c = cap;
   if (c < 1) c = 1;
