@@ -36,6 +36,11 @@ constexpr int kPT = 64 * kPW;          // threads per workgroup
 constexpr int kPlaneMaxW = 256;        // level-0 row width (one float4 per lane)
 constexpr int kPlaneMaxMW = 128;       // level-1 output width (two columns per lane)
 constexpr int kPlaneLdsCap = 160 * 1024 - 1024;
+// noisy wave-chunk level 1 with the halo rows of the boundaries where a pair of waves starts
+// computed once (bidirectional chunks); WAM_PLANE_SHARE=0 builds the one-direction form for A/B
+#ifndef WAM_PLANE_SHARE
+#define WAM_PLANE_SHARE 1
+#endif
 
 struct PlaneGeom {
   int J;
@@ -70,6 +75,15 @@ struct BandOut {
     }
   }
 };
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, class F>
+__device__ __forceinline__ void plane_static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    plane_static_for<B + 1, E>(f);
+  }
+}
 
 __device__ __forceinline__ float wave_max(float m) {
 #pragma unroll
@@ -365,6 +379,18 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     const int i1 = min(mh, i0 + R);
     const int er0 = 2 * i0 - p;
     const int T = i1 > i0 ? 2 * (i1 - i0) + L - 2 : 0;
+    // SHARE (noisy analysis): even waves stream their chunk bottom-up, odd waves top-down, so the
+    // waves 2k and 2k + 1 both START at their common boundary b: each computes three of the L - 2
+    // ext rows both need (2b-6 .. 2b-1 at L = 8) and takes the other three from its partner through
+    // the LL_1 area of LDS (empty until the first emit), instead of both computing all six -- a
+    // quarter of the halo rows (each row is fetched, noised and filtered once per wave that needs
+    // it). Local step s runs 0 .. T-1 over the wave's ext rows in its own direction; ring slot s % L.
+    constexpr bool SHARE = WAM_PLANE_SHARE && NOISE && MC == 0 && L >= 4 && NBL == 2;
+    constexpr int HS = (L - 2) / 2;  // shared rows computed by each wave of a pair
+    const bool up = SHARE && !(wv & 1);
+    const int pw = wv ^ 1;  // partner
+    // both waves of the pair have rows, and the LL_1 area (J > 1) holds the exchange
+    const bool share = SHARE && T > 0 && pw * R < mh && g.llcap >= kPW * HS * 2 * CPL * 64;
     float mx[4] = {0.f, 0.f, 0.f, 0.f};
     const float2* hsrc[CPL];
 #pragma unroll
@@ -374,7 +400,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     RowRegs<4, 1> f[NBL][NCH];
     int srow[NBL];
     auto fetch = [&](RowRegs<4, 1> (&fr)[NCH], int& sr_out, int t) {
-      const int sr = row_src(er0 + t, nh, mode);
+      const int sr = row_src(up ? 2 * i1 - 1 - t : er0 + t, nh, mode);
       const bool valid = sr >= 0;
       const int rr = valid ? sr : 0;
       sr_out = sr;  // -1: zero row
@@ -424,8 +450,9 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
       for (int c = 0; c < CPL; ++c) rv[c][slot] = acc[c];
       wsync();
     };
-    // output row i from ring slots (s0 + k) % L, k = 0 .. L-1
-    auto emit = [&](int i, int s0) {
+    // output row i from ring slots (s0 + k) % L, k = 0 .. L-1 (REV: bottom-up wave, tap k in slot
+    // (s0 + L - 1 - k) % L); the fma chain is tap 0 .. L-1 either way
+    auto emit_dir = [&](auto rev, int i, int s0) {
       f2 av[CPL], hd[CPL];
 #pragma unroll
       for (int c = 0; c < CPL; ++c) av[c] = hd[c] = f2{0.f, 0.f};
@@ -433,7 +460,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
       for (int k = 0; k < L; ++k) {
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
-          const f2 r = rv[c][(s0 + k) % L];
+          const f2 r = rv[c][decltype(rev)::value ? (s0 + L - 1 - k) % L : (s0 + k) % L];
           av[c] = __builtin_elementwise_fma(f2{fh2[k].x, fh2[k].x}, r, av[c]);  // (a, v) = sum flo[k] * (lo, hi)
           hd[c] = __builtin_elementwise_fma(f2{fh2[k].y, fh2[k].y}, r, hd[c]);  // (h, d) = sum fhi[k] * (lo, hi)
         }
@@ -441,7 +468,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
         const int j = lane + 64 * c;
-        if (j < mw && i < i1) {
+        if (j < mw && i >= i0 && i < i1) {  // a partial last group: rows outside the chunk
           const int64_t idx = (int64_t)i * mw + j;
           if (lastlvl) bo.put(g, g.off_a, bn, idx, av[c].x, mx[3]);
           else bufA[idx] = av[c].x;
@@ -451,21 +478,65 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
         }
       }
     };
+    // after local step s = L-1 + 2m: output row i0 + m (top-down) or i1 - 1 - m (bottom-up)
+    auto emit = [&](int m, int s0) {
+      if (up) emit_dir(std::true_type{}, i1 - 1 - m, s0);
+      else emit_dir(std::false_type{}, i0 + m, s0);
+    };
 
     // Every fetch is unconditional (rows past the chunk are clamped to valid source rows and never
     // emitted): loads under divergent control flow would make the compiler drain vmcnt to 0 at the
     // join, serialising the row stream on memory latency.
+    float za[4] = {0.f, 0.f, 0.f, 0.f}, zb[4] = {0.f, 0.f, 0.f, 0.f};
     if (T > 0) {
 #pragma unroll
       for (int u = 0; u < NBL - 1; ++u) fetch(f[u], srow[u], u);
-      // prologue: ext rows 0 .. L-3 fill ring slots 0 .. L-3
-      float za[4] = {0.f, 0.f, 0.f, 0.f}, zb[4] = {0.f, 0.f, 0.f, 0.f};
+    }
+    // prologue: ext rows 0 .. L-3 fill ring slots 0 .. L-3 (SHARE: rows HS .. L-3 come from the
+    // partner between two workgroup barriers that every wave executes)
+    auto prologue_step = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      fetch(f[(t + NBL - 1) % NBL], srow[(t + NBL - 1) % NBL], t + NBL - 1);
+      if (!(t & 1)) noise2(za, zb, srow[t % NBL], srow[(t + 1) % NBL]);  // row t + 1 is fetched
+      consume(f[t % NBL], srow[t % NBL], t, (t & 1) ? zb : za);
+    };
+    if constexpr (SHARE) {
+      if (T > 0) {
+        plane_static_for<0, HS - 1>([&](auto tc) { prologue_step(tc); });
+        constexpr int t = HS - 1;  // last computed shared row
+        if (share) {
+          // no fetch of row HS: its slot takes row L-2, the first row after the exchange
+          if (!(t & 1)) noise2(za, zb, srow[t % NBL], srow[t % NBL]);
+          consume(f[t % NBL], srow[t % NBL], t, (t & 1) ? zb : za);
+          fetch(f[(L - 2) % NBL], srow[(L - 2) % NBL], L - 2);
+          float* xw = bufA + wv * (HS * 2 * CPL * 64);
 #pragma unroll
-      for (int t = 0; t < L - 2; ++t) {
-        fetch(f[(t + NBL - 1) % NBL], srow[(t + NBL - 1) % NBL], t + NBL - 1);
-        if (!(t & 1)) noise2(za, zb, srow[t % NBL], srow[(t + 1) % NBL]);  // row t + 1 is fetched
-        consume(f[t % NBL], srow[t % NBL], t, (t & 1) ? zb : za);
+          for (int s = 0; s < HS; ++s)
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+              xw[((s * CPL + c) * 2) * 64 + lane] = rv[c][s].x;
+              xw[((s * CPL + c) * 2 + 1) * 64 + lane] = rv[c][s].y;
+            }
+        } else {
+          prologue_step(std::integral_constant<int, t>{});
+        }
       }
+      __syncthreads();  // the partners' shared rows are in LDS
+      if (share) {
+        // partner's step s is this wave's step L-3-s (the pair streams the rows in opposite orders)
+        const float* xp = bufA + pw * (HS * 2 * CPL * 64);
+#pragma unroll
+        for (int s = 0; s < HS; ++s)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c)
+            rv[c][L - 3 - s] = f2{xp[((s * CPL + c) * 2) * 64 + lane], xp[((s * CPL + c) * 2 + 1) * 64 + lane]};
+      }
+      __syncthreads();  // every exchange read precedes the first LL_1 row written over the area
+      if (T > 0 && !share) plane_static_for<HS, L - 2>([&](auto tc) { prologue_step(tc); });
+    } else if (T > 0) {
+      plane_static_for<0, L - 2>([&](auto tc) { prologue_step(tc); });
+    }
+    if (T > 0) {
       // steady state: GRPL ext rows per iteration; t = base + u with base = L-2 (mod GRPL), so
       // t % L and t % NBL are compile-time constants; a partial last group computes output rows
       // >= i1, which emit() drops
@@ -478,7 +549,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
             noise2(za, zb, srow[(L - 2 + u) % NBL], srow[(L - 2 + u + 1) % NBL]);
           consume(f[(L - 2 + u) % NBL], srow[(L - 2 + u) % NBL], (L - 2 + u) % L, (u & 1) ? zb : za);
           // after odd u: output row (t - (L-1)) / 2 from ext rows t-L+1 .. t = slots (u-1+k) % L
-          if (u & 1) emit(i0 + (t - (L - 1)) / 2, (u - 1) % L);
+          if (u & 1) emit((t - (L - 1)) / 2, (u - 1) % L);
         }
       }
     }
