@@ -58,6 +58,8 @@ struct PlaneGeom {
   int sample_fast;                  // noisy analysis: logical order sample-fastest (1) or plane-fastest (0)
   int xcd_order;                    // workgroup ids through the XCD-aware swizzle (1) or as issued (0)
   int coop;                         // level 1 as the cooperative row stream (COOP kernels)
+  int xend;                         // noisy wave chunks: float offset in buffer B of the END-boundary
+                                    // exchange (-1: not allocated, halo rows computed by both waves)
 };
 
 template <bool MAPS>
@@ -391,6 +393,14 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     const int pw = wv ^ 1;  // partner
     // both waves of the pair have rows, and the LL_1 area (J > 1) holds the exchange
     const bool share = SHARE && T > 0 && pw * R < mh && g.llcap >= kPW * HS * 2 * CPL * 64;
+    // END boundaries (waves 2k-1 top-down | 2k bottom-up) meet at the end of both streams: each
+    // computes the first HS of the L - 2 shared rows (its steps T-L+2 .. T-HS-1) and takes the rest
+    // from its partner through buffer B (g.xend) after one workgroup barrier. Both waves need
+    // >= L - 2 + 2*HS steps so that the START and END shared rows do not overlap.
+    const int pe = (wv & 1) ? wv + 1 : wv - 1;
+    const int pe_rows = (pe >= 0 && pe < kPW) ? max(0, min(mh, (pe + 1) * R) - pe * R) : 0;
+    const bool end_share = SHARE && g.xend >= 0 && T >= 2 * (L - 2) && 2 * pe_rows + L - 2 >= 2 * (L - 2);
+    const int T_stop = end_share ? T - HS : T;  // the loop's last step + 1
     float mx[4] = {0.f, 0.f, 0.f, 0.f};
     const float2* hsrc[CPL];
 #pragma unroll
@@ -540,10 +550,13 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
       // steady state: GRPL ext rows per iteration; t = base + u with base = L-2 (mod GRPL), so
       // t % L and t % NBL are compile-time constants; a partial last group computes output rows
       // >= i1, which emit() drops
-      for (int base = L - 2; base < T; base += GRPL) {
+      for (int base = L - 2; base < T_stop; base += GRPL) {
 #pragma unroll
         for (int u = 0; u < GRPL; ++u) {
           const int t = base + u;
+          if constexpr (SHARE) {
+            if (t >= T_stop) break;  // uniform: no garbage steps past the chunk
+          }
           fetch(f[(L - 2 + u + NBL - 1) % NBL], srow[(L - 2 + u + NBL - 1) % NBL], t + NBL - 1);
           if (!(u & 1))  // t even (L - 2 and GRPL are even): rows t, t + 1 noised together
             noise2(za, zb, srow[(L - 2 + u) % NBL], srow[(L - 2 + u + 1) % NBL]);
@@ -551,6 +564,56 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
           // after odd u: output row (t - (L-1)) / 2 from ext rows t-L+1 .. t = slots (u-1+k) % L
           if (u & 1) emit((t - (L - 1)) / 2, (u - 1) % L);
         }
+      }
+    }
+    if constexpr (SHARE) {
+      // END exchange: this wave's rows of steps T-L+2 .. T-HS-1 out, its partner's (which are this
+      // wave's steps T-1 .. T-HS, in the opposite order) in; then the last HS/2+... outputs. T % L
+      // is even and fixes every ring slot: one static case per residue.
+      constexpr int XR = HS * 2;  // floats per column of one direction (rows x (lo, hi))
+      const int mw1 = g.mw[0];
+      const int xb = (((wv & 1) ? (wv - 1) / 2 : (wv - 2) / 2) * 2) * XR * mw1;  // this boundary's block
+      float* xme = bufB + g.xend + xb + (wv & 1) * XR * mw1;
+      const float* xpe = bufB + g.xend + xb + (pe & 1) * XR * mw1;
+      auto by_residue = [&](auto body) {
+        plane_static_for<0, L / 2>([&](auto rc) {
+          constexpr int R0 = 2 * decltype(rc)::value;
+          if (T % L == R0) body(std::integral_constant<int, R0>{});
+        });
+      };
+      if (end_share) {
+        by_residue([&](auto rc) {
+          constexpr int R0 = decltype(rc)::value;
+#pragma unroll
+          for (int k = 0; k < HS; ++k)
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+              const int j = lane + 64 * c;
+              if (j < mw1) {
+                const f2 v = rv[c][(R0 + 2 * L - (L - 2) + k) % L];  // step T-(L-2)+k
+                xme[(2 * k) * mw1 + j] = v.x;
+                xme[(2 * k + 1) * mw1 + j] = v.y;
+              }
+            }
+        });
+      }
+      __syncthreads();  // every END pair's rows are in buffer B
+      if (end_share) {
+        by_residue([&](auto rc) {
+          constexpr int R0 = decltype(rc)::value;
+          // received steps in stream order (T-HS .. T-1), each output emitted right after its last
+          // step as in the loop -- a later step's row takes the ring slot an earlier output reads
+#pragma unroll
+          for (int k = HS - 1; k >= 0; --k) {  // partner's row k = this wave's step T-1-k
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+              const int j = min(lane + 64 * c, mw1 - 1);  // lanes past the row: a duplicate, never stored
+              rv[c][(R0 + 2 * L - 1 - k) % L] = f2{xpe[(2 * k) * mw1 + j], xpe[(2 * k + 1) * mw1 + j]};
+            }
+            if (k & 1) continue;  // step T-1-k is odd when k is even (T even)
+            emit((T - 1 - k - (L - 1)) / 2, (R0 + 2 * L - 1 - k - (L - 1)) % L);
+          }
+        });
       }
     }
     if constexpr (MAPS) {
@@ -790,7 +853,7 @@ bool coop_ok(const wam_plan* p, int nw0, bool noisy = false) {
   return (int64_t)coop_lds_floats(p, nw0, rowlds, llcap) * 4 <= kTwoWgLds || (p->flags & WAM_PLAN_FORCE_COOP);
 }
 
-int lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap, bool noisy = false) {
+int lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap, bool noisy = false, int* xend = nullptr) {
   if (coop_ok(p, nw0, noisy)) return coop_lds_floats(p, nw0, rowlds, llcap);
   rowlds = kPadL + 256 + 8;  // commit covers 256 samples; pads <= p + 2 <= 20 fit behind them
   if (rowlds < kPadL + nw0 + p->pad + 4) rowlds = kPadL + nw0 + p->pad + 4;
@@ -799,9 +862,21 @@ int lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap, bool noisy =
   // misaligned b128/b64 LDS access is split by the hardware and made this kernel 3x slower
   llcap = p->levels > 1 ? (int)((p->lout[0][0] * p->lout[0][1] + 63) & ~63) : 0;
   int64_t bcap = (int64_t)kPW * rowlds;
+  int64_t ll2 = 0;
   if (p->levels > 1) {
-    const int64_t ll2 = p->lout[1][0] * p->lout[1][1];
+    ll2 = p->lout[1][0] * p->lout[1][1];
     if (ll2 > bcap) bcap = ll2;
+  }
+  if (xend) *xend = -1;
+  if (noisy && WAM_PLANE_SHARE) {
+    // the END-boundary exchange behind the wave rows: (kPW/2 - 1) boundaries x 2 directions x
+    // (L-2)/2 rows x (lo, hi) x mw floats, if two workgroups still fit a CU
+    const int64_t xe = (int64_t)(kPW / 2 - 1) * 2 * (p->L - 2) * p->lout[0][1];
+    const int64_t b2 = std::max<int64_t>((int64_t)kPW * rowlds + xe, ll2);
+    if ((llcap + b2) * 4 + 4 * WAM_MAX_BANDS + 64 <= 160 * 1024 / 2) {
+      if (xend) *xend = kPW * rowlds;
+      bcap = b2;
+    }
   }
   return (int)(llcap + bcap);
 }
@@ -834,7 +909,7 @@ PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items
   g.nbands = p->nbands;
   g.items_total = items_total;
   g.maps_item = p->band_off[p->nbands];
-  lds_floats(p, nw0, g.rowlds, g.llcap, noisy);
+  lds_floats(p, nw0, g.rowlds, g.llcap, noisy, &g.xend);
   g.coop = coop_ok(p, nw0, noisy);
   // noisy analysis: sample-fastest through the XCD swizzle (the S samples of a plane read it from
   // one L2; plane-fastest and un-swizzled orders measured 684 / 681 vs 666 us,

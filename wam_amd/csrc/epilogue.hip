@@ -171,14 +171,13 @@ __global__ void __launch_bounds__(kSigT) k_item_sigma_split(const float* __restr
   }
 }
 
-// ranges per item: >= 32 K floats per range (the arrivals on an item's counter are serialised at
-// the memory side: short ranges of many workgroups queue there -- c2 with 32 ranges of 4.7 K
-// floats per image ran 21 us), but at least ~512 workgroups over the call and >= 4 K floats each
+// ranges per item: about 2,048 workgroups over the call (every CU a few ranges, so the loads of
+// one range overlap the next's), each range >= 8 K floats so that an item's arrivals on its counter
+// (serialised at the memory side) stay few: c2 at 32 ranges of 4.7 K floats per image ran 21 us,
+// 18 ranges of 8.4 K run at the copy rate (profiles/r05f_sigma_split.log)
 void sigma_split(int64_t items, int64_t len, bool vec4, int64_t& chunk, int& chunks) {
-  int64_t c = (len + 32767) / 32768;
-  const int64_t fill = (512 + items - 1) / items;
-  if (c < fill) c = fill;
-  const int64_t cap = len / 4096 > 1 ? len / 4096 : 1;
+  int64_t c = (2048 + items - 1) / items;
+  const int64_t cap = len / 8192 > 1 ? len / 8192 : 1;
   if (c > cap) c = cap;
   if (c < 1) c = 1;
   chunk = (len + c - 1) / c;
