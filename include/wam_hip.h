@@ -217,6 +217,14 @@ int wam_frame_trapz(int64_t groups, int64_t k0, int64_t group_items, int64_t fra
                     const float* band_max, int n_bands, int normalize, const float* weights,
                     float* prev, float* acc, void* stream);
 
+/* wam_frame_trapz in coefficient order (dst / cband as for wam_frame_accumulate_coef): the maps
+ * are read as contiguous rows, prev / acc go through the mosaic. Pixels outside the mosaic are not
+ * touched -- their G is 0, so with prev == 0 there (zero-initialised, as wam_amd/wam_2D.py passes
+ * them) the result is bit-identical to wam_frame_trapz. */
+int wam_frame_trapz_coef(int64_t groups, int64_t k0, int64_t group_items, int64_t maps_item_len, int64_t frame_len,
+                         const int32_t* dst, const int32_t* cband, const float* maps, const float* band_max,
+                         int n_bands, int normalize, const float* weights, float* prev, float* acc, void* stream);
+
 /* 3D cube (lib/wam_3D.py:127-166 refactor; :585-587 legacy averaging; :638 IG trapezoid):
  * value = maps[item, src[p]] with maps = |coeff grads| from wam_subband_maps(channels = 1)
  * (no channel mean, no normalisation). For s in [0, groups) in order:

@@ -26,3 +26,38 @@ def test_coef_order_equals_gather(wav, frame, normalize):
     check(lib.wam_frame_accumulate(groups, n, src.numel(), ptr(src), ptr(band), ptr(maps), p.coeff_numel, ptr(bmax),
                                    p.nbands, int(normalize), ptr(b), stream_of(b.device)))
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("shape,wav,J", [(224, "db4", 3), (512, "sym8", 5)])
+@pytest.mark.parametrize("normalize", [True, False])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_trapz_coef_order_equals_gather(shape, wav, J, normalize, weighted):
+    """wam_frame_trapz_coef (the IG path's trapezoid) vs the per-pixel wam_frame_trapz over two
+    chained passes (k0 = 0, then k0 > 0 carrying prev), NaN / inf map values included: bit-identical
+    fp32 acc and prev. 512^2 sym8 J=5 takes the runs-of-items branch (mosaic tables > 2 MB)."""
+    from wam_amd import frames, plan as P
+    from wam_amd._lib import check, lib, ptr, stream_of
+    p = P.get_plan(2, (shape, shape), J, wav, "reflect", "cuda")
+    n = 6
+    _, gmap, (rh, rw) = frames.ig_frames(p, n, "native", "cuda")
+    assert P._inverse_map(gmap, p.coeff_numel) is not None
+    src, band = gmap
+    torch.manual_seed(5)
+    acc_a = torch.zeros(n * rh * rw, device="cuda")
+    prev_a = torch.zeros_like(acc_a)
+    acc_b, prev_b = acc_a.clone(), prev_a.clone()
+    k0 = 0
+    for groups in (11, 5):
+        maps = torch.rand(groups * n * p.coeff_numel, device="cuda")
+        maps[::997] = float("nan")
+        maps[5::1999] = float("inf")
+        bmax = torch.rand(groups, p.nbands, device="cuda") + 0.5
+        w = torch.rand(groups, device="cuda") if weighted else None
+        P.frame_trapz(groups, k0, n, gmap, maps, p.coeff_numel, bmax, p.nbands, normalize, prev_a, acc_a, w)
+        check(lib.wam_frame_trapz(groups, k0, n, src.numel(), ptr(src), ptr(band), ptr(maps), p.coeff_numel,
+                                  ptr(bmax), p.nbands, int(normalize), ptr(w), ptr(prev_b), ptr(acc_b),
+                                  stream_of(acc_b.device)))
+        k0 += groups
+    torch.cuda.synchronize()
+    assert torch.equal(acc_a, acc_b) and torch.equal(prev_a, prev_b)
+    assert acc_a.abs().sum() > 0

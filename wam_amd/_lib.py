@@ -56,6 +56,8 @@ _SIGS = {
                                           c_vp]),
     "wam_frame_trapz": (c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_vp, c_vp,
                                 c_vp, c_vp]),
+    "wam_frame_trapz_coef": (c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp,
+                                     c_vp, c_vp, c_vp]),
     "wam_cube_accumulate": (c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_int, c_f32, c_vp, c_vp, c_vp,
                                     c_vp]),
     "wam_accumulate_f32": (c_int, [c_i64, c_i64, c_vp, c_f32, c_vp, c_vp]),

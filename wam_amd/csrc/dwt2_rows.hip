@@ -193,7 +193,10 @@ __global__ void __launch_bounds__(256) k_ana_rows(const float* __restrict__ in, 
       rl[c][L - 2] = lo[c];
       rh[c][L - 2] = hi[c];
     }
-    fetch(f[0], nzv[0], er + 2);  // one row past the chunk on the last iteration: harmless (clamped)
+    // on the last iteration the row after the chunk is never used: re-fetch the chunk's last ext
+    // row (a cache hit) instead of the next chunk's first row (an HBM re-read: that chunk's wave
+    // fetched it long before)
+    fetch(f[0], nzv[0], min(er + 2, er0 + 2 * (i1 - i0) + L - 3));
     process(f[1], nzv[1], lo, hi);
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
@@ -402,7 +405,7 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
         rl[c][q][L - 2] = lo[c][q];
         rh[c][q][L - 2] = hi[c][q];
       }
-    fetch(f[0], er + 2);
+    fetch(f[0], min(er + 2, er0 + 2 * (i1 - i0) + L - 3));  // past the chunk: its last row (see k_ana_rows)
     process(f[1], lo, hi);
 #pragma unroll
     for (int c = 0; c < C; ++c)

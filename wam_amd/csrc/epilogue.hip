@@ -365,7 +365,9 @@ __global__ void __launch_bounds__(256) k_frame_accumulate_coef(int64_t groups, i
   // once per item
   const int64_t mstride = group_items * maps_item_len;
   const int64_t runs = (group_items + items_per_thread - 1) / items_per_thread;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < runs * maps_item_len;
+  // XCD-aware block order: the cache lines two neighbouring blocks share (item rows are not
+  // line-aligned) are fetched into one XCD's L2 instead of two
+  for (int64_t t = wam_xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x; t < runs * maps_item_len;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = t / maps_item_len;
     const int64_t k = t - r * maps_item_len;
@@ -446,6 +448,65 @@ __global__ void __launch_bounds__(256) k_frame_trapz(int64_t groups, int64_t k0,
     for (; s < groups; ++s) step(s, mp[s * mstride], normalize ? band_max[s * n_bands + b] : 1.f);
     acc[t] = a;
     prev[t] = pv;
+  }
+}
+
+// k_frame_trapz in COEFFICIENT order (see k_frame_accumulate_coef): thread per (coefficient k,
+// run of items), maps read as contiguous rows, the fp32 frame (acc, prev) addressed through the
+// injective mosaic. Pixels outside the mosaic are never touched: the pixel-order kernel adds
+// (0 + 0) / 2 or w * 0 to their zero-initialised sums, i.e. leaves them as they are. Per pixel the
+// step order and arithmetic are those of k_frame_trapz (bit-identical).
+__global__ void __launch_bounds__(256) k_frame_trapz_coef(int64_t groups, int64_t k0, int64_t group_items,
+                                                          int64_t maps_item_len, int64_t frame_len,
+                                                          const int32_t* __restrict__ dst,
+                                                          const int32_t* __restrict__ cband,
+                                                          const float* __restrict__ maps,
+                                                          const float* __restrict__ band_max, int n_bands,
+                                                          int normalize, const float* __restrict__ weights,
+                                                          int64_t items_per_thread, float* __restrict__ prev,
+                                                          float* __restrict__ acc) {
+  const int64_t mstride = group_items * maps_item_len;
+  const int64_t runs = (group_items + items_per_thread - 1) / items_per_thread;
+  // XCD-aware block order: the cache lines two neighbouring blocks share (item rows are not
+  // line-aligned) are fetched into one XCD's L2 instead of two
+  for (int64_t t = wam_xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x; t < runs * maps_item_len;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / maps_item_len;
+    const int64_t k = t - r * maps_item_len;
+    const int32_t d = dst[k];
+    if (d < 0) continue;
+    const int32_t b = cband[k];
+    const int64_t n1 = min(group_items, (r + 1) * items_per_thread);
+    for (int64_t n = r * items_per_thread; n < n1; ++n) {
+      const int64_t fi = n * frame_len + d;
+      float a = acc[fi];
+      float pv = prev[fi];
+      const float* mp = maps + n * maps_item_len + k;
+      auto step = [&](int64_t s, float v, float m) {
+        if (normalize) v = v / m;
+        v = nan_to_num(v);
+        if (weights) {
+          a = fmaf(weights[s], v, a);
+        } else {
+          if (k0 + s > 0) a = a + (pv + v) / 2.0f;
+          pv = v;
+        }
+      };
+      int64_t s = 0;
+      for (; s + 8 <= groups; s += 8) {
+        float v[8], m[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          v[u] = mp[(s + u) * mstride];
+          m[u] = normalize ? band_max[(s + u) * n_bands + b] : 1.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) step(s + u, v[u], m[u]);
+      }
+      for (; s < groups; ++s) step(s, mp[s * mstride], normalize ? band_max[s * n_bands + b] : 1.f);
+      acc[fi] = a;
+      prev[fi] = pv;
+    }
   }
 }
 
@@ -799,6 +860,27 @@ int wam_frame_accumulate_coef(int64_t groups, int64_t group_items, int64_t maps_
   hipLaunchKernelGGL(k_frame_accumulate_coef, dim3(wam_grid(threads, 256)), dim3(256), 0, (hipStream_t)stream, groups,
                      group_items, maps_item_len, frame_len, dst, cband, maps, band_max, n_bands, normalize, ipt,
                      frame);
+  WAM_LAUNCH_CHECK();
+  return WAM_OK;
+}
+
+int wam_frame_trapz_coef(int64_t groups, int64_t k0, int64_t group_items, int64_t maps_item_len, int64_t frame_len,
+                         const int32_t* dst, const int32_t* cband, const float* maps, const float* band_max,
+                         int n_bands, int normalize, const float* weights, float* prev, float* acc, void* stream) {
+  if (groups < 0 || group_items < 0 || maps_item_len < 0 || frame_len < 0 || !dst || !cband || !maps || !prev || !acc)
+    return WAM_ERR_INVALID_ARG;
+  if (normalize && !band_max) return WAM_ERR_INVALID_ARG;
+  const int64_t work = group_items * maps_item_len;
+  if (work == 0 || groups == 0) return WAM_OK;
+  WamTimer tm((hipStream_t)stream, "k_frame_trapz_coef",
+              4.0 * (double)groups * group_items * frame_len + 16.0 * group_items * frame_len + 8.0 * frame_len);
+  // runs of items per thread as in wam_frame_accumulate_coef (mosaic tables read once per run)
+  int64_t ipt = maps_item_len * 8 > (int64_t(2) << 20) ? work / (int64_t(1) << 20) : 1;
+  ipt = ipt < 1 ? 1 : (ipt > group_items ? group_items : ipt);
+  const int64_t threads = (group_items + ipt - 1) / ipt * maps_item_len;
+  hipLaunchKernelGGL(k_frame_trapz_coef, dim3(wam_grid(threads, 256)), dim3(256), 0, (hipStream_t)stream, groups, k0,
+                     group_items, maps_item_len, frame_len, dst, cband, maps, band_max, n_bands, normalize, weights,
+                     ipt, prev, acc);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }

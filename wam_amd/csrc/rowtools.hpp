@@ -248,7 +248,9 @@ __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float s
         rh[ns] = fok[uf] ? sd * fh[uf] : 0.f;
         rv[ns] = fok[uf] ? sd * fv[uf] : 0.f;
         rd[ns] = fok[uf] ? sd * fd[uf] : 0.f;
-        fetch(uf, q + PF);  // past the chunk: clamped, never used
+        // rows past the chunk are never used: re-fetch the chunk's last row (a cache hit) rather
+        // than the next chunk's first rows, which that chunk's wave read long ago (HBM re-reads)
+        fetch(uf, min(q + PF, qend - 1));
         f2 lo = {0.f, 0.f}, hi = {0.f, 0.f};  // (lo0, lo1), (hi0, hi1)
   #pragma unroll
         for (int i2 = 0; i2 < H2; ++i2) {
@@ -324,7 +326,7 @@ __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float s
         rh[H2 - 1] = fok[u] ? sd * fh[u] : 0.f;
         rv[H2 - 1] = fok[u] ? sd * fv[u] : 0.f;
         rd[H2 - 1] = fok[u] ? sd * fd[u] : 0.f;
-        fetch(u, q + PF);  // past the chunk: clamped, never used
+        fetch(u, min(q + PF, qend - 1));  // past the chunk: the chunk's last row again (see PK)
         float lo0 = 0.f, lo1 = 0.f, hi0 = 0.f, hi1 = 0.f;
   #pragma unroll
         for (int i2 = 0; i2 < H2; ++i2) {

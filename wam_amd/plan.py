@@ -286,6 +286,12 @@ def frame_accumulate(groups, group_items, gmap, maps, maps_item_len, band_max, n
 def frame_trapz(groups, k0, group_items, gmap, maps, maps_item_len, band_max, n_bands, normalize, prev, acc,
                 weights=None):
     src, band = gmap
+    inv = _inverse_map(gmap, maps_item_len)
+    if inv is not None:  # coefficient order: contiguous map reads (prev / acc are zero outside the mosaic)
+        check(lib.wam_frame_trapz_coef(groups, k0, group_items, maps_item_len, src.numel(), ptr(inv[0]),
+                                       ptr(inv[1]), ptr(maps), ptr(band_max), n_bands, int(bool(normalize)),
+                                       ptr(weights), ptr(prev), ptr(acc), stream_of(acc.device)))
+        return
     check(lib.wam_frame_trapz(groups, k0, group_items, src.numel(), ptr(src), ptr(band), ptr(maps), maps_item_len,
                               ptr(band_max), n_bands, int(bool(normalize)), ptr(weights), ptr(prev), ptr(acc),
                               stream_of(acc.device)))
