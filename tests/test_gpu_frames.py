@@ -34,11 +34,11 @@ def test_coef_order_equals_gather(wav, frame, normalize):
 def test_trapz_coef_order_equals_gather(shape, wav, J, normalize, weighted):
     """wam_frame_trapz_coef (the IG path's trapezoid) vs the per-pixel wam_frame_trapz over two
     chained passes (k0 = 0, then k0 > 0 carrying prev), NaN / inf map values included: bit-identical
-    fp32 acc and prev. 512^2 sym8 J=5 takes the runs-of-items branch (mosaic tables > 2 MB)."""
+    fp32 acc and prev. 512^2 sym8 J=5 takes the runs-of-items branch (mosaic tables > 2 MB, n * K / 2^22 = 2)."""
     from wam_amd import frames, plan as P
     from wam_amd._lib import check, lib, ptr, stream_of
     p = P.get_plan(2, (shape, shape), J, wav, "reflect", "cuda")
-    n = 6
+    n = 6 if shape == 224 else 32  # 32 x 293 K coefficients: 2 items per thread (runs branch)
     _, gmap, (rh, rw) = frames.ig_frames(p, n, "native", "cuda")
     assert P._inverse_map(gmap, p.coeff_numel) is not None
     src, band = gmap

@@ -365,9 +365,7 @@ __global__ void __launch_bounds__(256) k_frame_accumulate_coef(int64_t groups, i
   // once per item
   const int64_t mstride = group_items * maps_item_len;
   const int64_t runs = (group_items + items_per_thread - 1) / items_per_thread;
-  // XCD-aware block order: the cache lines two neighbouring blocks share (item rows are not
-  // line-aligned) are fetched into one XCD's L2 instead of two
-  for (int64_t t = wam_xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x; t < runs * maps_item_len;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < runs * maps_item_len;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = t / maps_item_len;
     const int64_t k = t - r * maps_item_len;
@@ -467,8 +465,9 @@ __global__ void __launch_bounds__(256) k_frame_trapz_coef(int64_t groups, int64_
                                                           float* __restrict__ acc) {
   const int64_t mstride = group_items * maps_item_len;
   const int64_t runs = (group_items + items_per_thread - 1) / items_per_thread;
-  // XCD-aware block order: the cache lines two neighbouring blocks share (item rows are not
-  // line-aligned) are fetched into one XCD's L2 instead of two
+  // XCD-aware block order: a thread's run of items and the neighbouring runs of the same
+  // coefficients land on one XCD, whose L2 then holds the mosaic tables and the lines shared by
+  // neighbouring blocks (c4 trapezoid PMC/algorithmic 1.19 without it, 1.07 with it)
   for (int64_t t = wam_xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x; t < runs * maps_item_len;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = t / maps_item_len;
@@ -874,8 +873,11 @@ int wam_frame_trapz_coef(int64_t groups, int64_t k0, int64_t group_items, int64_
   if (work == 0 || groups == 0) return WAM_OK;
   WamTimer tm((hipStream_t)stream, "k_frame_trapz_coef",
               4.0 * (double)groups * group_items * frame_len + 16.0 * group_items * frame_len + 8.0 * frame_len);
-  // runs of items per thread as in wam_frame_accumulate_coef (mosaic tables read once per run)
-  int64_t ipt = maps_item_len * 8 > (int64_t(2) << 20) ? work / (int64_t(1) << 20) : 1;
+  // runs of items per thread when the mosaic tables outgrow L2 (as in wam_frame_accumulate_coef),
+  // sized for ~4 M threads: c4 (128 images x 293 K coefficients) runs 9 items per thread --
+  // PMC/algorithmic 1.058 and 929 us per 21-step launch, against 1.066 / 1,007 us at ~1 M threads
+  // and 1.133 / 1,066 us at one item per thread (profiles/r05o_trapz_runs_ab.log)
+  int64_t ipt = maps_item_len * 8 > (int64_t(2) << 20) ? work / (int64_t(1) << 22) : 1;
   ipt = ipt < 1 ? 1 : (ipt > group_items ? group_items : ipt);
   const int64_t threads = (group_items + ipt - 1) / ipt * maps_item_len;
   hipLaunchKernelGGL(k_frame_trapz_coef, dim3(wam_grid(threads, 256)), dim3(256), 0, (hipStream_t)stream, groups, k0,
