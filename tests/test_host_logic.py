@@ -406,3 +406,32 @@ def test_wam_group_budget():
     assert wam_group(2, 64, per, budget_bytes=36 << 30) == 28
     assert wam_group(2, 5, per, budget_bytes=36 << 30) == 5
     assert wam_group(4, 64, 100 << 30, budget_bytes=8 << 30) == 4
+
+
+def test_profiling_phase_ranges(monkeypatch):
+    """wam_amd.profiling.phase: a no-op unless WAM_PROFILE=1; when on, each phase pushes and pops one
+    roctx range named wam:<name>, also when the body raises (CPU: a stand-in for the roctx library)."""
+    from wam_amd import profiling
+    calls = []
+
+    class FakeRoctx:
+        def roctxRangePushA(self, s):
+            calls.append(("push", s))
+            return 0
+
+        def roctxRangePop(self):
+            calls.append(("pop",))
+            return 0
+
+    monkeypatch.setattr(profiling, "ENABLED", False)
+    with profiling.phase("model"):
+        pass
+    assert calls == []
+    monkeypatch.setattr(profiling, "ENABLED", True)
+    monkeypatch.setattr(profiling, "_LIB", FakeRoctx())
+    with profiling.phase("model"):
+        pass
+    with pytest.raises(RuntimeError):
+        with profiling.phase("trapz"):
+            raise RuntimeError("x")
+    assert calls == [("push", b"wam:model"), ("pop",), ("push", b"wam:trapz"), ("pop",)]
