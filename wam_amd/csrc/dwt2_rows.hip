@@ -476,7 +476,10 @@ __global__ void __launch_bounds__(256) k_adj_maps(const float* __restrict__ in, 
 }
 
 // ------------------------------------------------------------------------------------------------
-constexpr int64_t kTargetWaves = 8192;
+// waves per launch the row chunking aims for: fewer, longer chunks re-read fewer halo rows (L - 2 ext
+// rows per chunk). 2,048 instead of 8,192: c4 wavedec same time, k_ana_rows PMC/algorithmic -11 %;
+// c4 adjoint maps level 1 164 -> 102 us at 2 x 128 images (profiles/r05s_ab_row_chunk_target.log)
+constexpr int64_t kTargetWaves = 2048;
 
 void pick_chunks(int64_t base, int mh, int& nchunks, int& R) {
   int64_t want = (kTargetWaves + base - 1) / base;
