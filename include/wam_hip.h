@@ -139,19 +139,6 @@ int wam_waverec_adjoint_maps(const wam_plan* plan, int64_t groups, int64_t group
                              const float* grad, float* maps, float* band_max, float* coeff_grads,
                              void* workspace, void* stream);
 
-/* wam_waverec_adjoint_maps (coeff_grads == NULL) with the maps written in FRAME order, i.e. already
- * placed on the reference's mosaic canvas (lib/wam_2D.py:233-261 visualize_grad_wam): band b's
- * |mean| value of coefficient (i, j) goes to maps[image, (rects[4b] + i) * frame_w + rects[4b+1] + j]
- * when i < rects[4b+2] and j < rects[4b+3] (the part of the band the mosaic shows; host array of
- * nbands x 4 int32, bands disjoint on the canvas); pixels no band shows are not written. band_max
- * covers every coefficient, as in wam_waverec_adjoint_maps. maps: [groups*group_items, frame_h *
- * frame_w]. The mosaic accumulation then reads each map once, contiguously (wam_frame_accumulate
- * with src[p] = p). WAM_ERR_UNSUPPORTED when the plane-resident kernel does not take the plan (the
- * caller uses wam_waverec_adjoint_maps + wam_frame_accumulate_coef instead). */
-int wam_waverec_adjoint_maps_frame(const wam_plan* plan, int64_t groups, int64_t group_items, int channels,
-                                   const float* grad, int frame_h, int frame_w, const int32_t* rects,
-                                   float* maps, float* band_max, void* stream);
-
 /* ------------------------------------------------------------------------------------------------
  * Live per-launch timing (profiling aid used by bench.py). While enabled every kernel launch is
  * bracketed by hipEventRecord on its stream and logged with its kernel name and ALGORITHMIC

@@ -61,38 +61,3 @@ def test_trapz_coef_order_equals_gather(shape, wav, J, normalize, weighted):
     torch.cuda.synchronize()
     assert torch.equal(acc_a, acc_b) and torch.equal(prev_a, prev_b)
     assert acc_a.abs().sum() > 0
-
-
-@pytest.mark.parametrize("wav,frame,hw", [("db4", "native", (224, 224)), ("haar", "legacy", (224, 224)),
-                                          ("db2", "native", (96, 128))])
-@pytest.mark.parametrize("normalize", [True, False])
-def test_canvas_order_maps_equal_coefficient_order(wav, frame, hw, normalize):
-    """wam_waverec_adjoint_maps_frame (the maps kernel writing each |mean| map straight onto the
-    mosaic canvas, the SmoothGrad classes' path) vs wam_waverec_adjoint_maps + the coefficient-order
-    accumulation: the same band maxima, every shown pixel's map value bit for bit, and the same fp64
-    frame after a 7-group accumulation."""
-    import numpy as np
-    from wam_amd import frames, plan as P
-    p = P.get_plan(2, hw, 3, wav, "reflect", "cuda")
-    n, groups, c = 5, 7, 3
-    gmap, (rh, rw) = frames.smooth_frame(p, n, frame, "cuda")
-    rects = frames.band_rects(p, gmap, (rh, rw))
-    assert rects is not None
-    torch.manual_seed(6)
-    g = torch.randn((groups * n * c,) + p.rec_shape, device="cuda")
-    maps_c, bmax_c, _ = p.adjoint_maps(g, groups, n, c)
-    mf = p.adjoint_maps_frame(g, groups, n, c, (rh, rw), rects[0])
-    assert mf is not None
-    maps_f, bmax_f = mf
-    assert torch.equal(bmax_c, bmax_f)
-    src, band = gmap
-    valid = src >= 0
-    mc = maps_c.view(groups * n, p.coeff_numel)[:, src[valid].long()]
-    mfv = maps_f.view(groups * n, rh * rw)[:, valid]
-    assert torch.equal(mc, mfv)
-    a = torch.zeros(n * rh * rw, dtype=torch.float64, device="cuda")
-    b = torch.zeros_like(a)
-    P.frame_accumulate(groups, n, gmap, maps_c, p.coeff_numel, bmax_c, p.nbands, normalize, a)
-    P.frame_accumulate_gather(groups, n, (rects[1], rects[2]), maps_f, rh * rw, bmax_f, p.nbands, normalize, b)
-    assert torch.equal(a, b)
-    assert int(np.count_nonzero(rects[0][:, 2] * rects[0][:, 3])) == p.nbands

@@ -60,12 +60,9 @@ struct PlaneGeom {
   int coop;                         // level 1 as the cooperative row stream (COOP kernels)
   int xend;                         // noisy wave chunks: float offset in buffer B of the END-boundary
                                     // exchange (-1: not allocated, halo rows computed by both waves)
-  int frame_w;                      // maps mode, > 0: maps in FRAME order (maps_item = frame pixels)
-  int fr[3 * WAM_MAX_LEVELS + 1][4];  // per 2D band: frame row, column of coefficient (0, 0), visible rows,
-                                    // visible columns (the reference mosaic's crop of the band)
 };
 
-template <bool MAPS, bool FRAME = false>
+template <bool MAPS>
 struct BandOut {
   float* out;
   int64_t item;
@@ -77,20 +74,6 @@ struct BandOut {
       mx = nan_max(mx, a);
     } else {
       out[g.items_total * off + item * numel + idx] = v;
-    }
-  }
-  // put() with the band index and the coefficient's (row, column): in frame-order maps mode the
-  // value goes to its mosaic pixel when the mosaic shows it (the maxima still cover every
-  // coefficient); otherwise exactly put()
-  __device__ __forceinline__ void put(const PlaneGeom& g, int band, int64_t off, int64_t numel, int64_t idx, int i,
-                                      int j, float v, float& mx) const {
-    if constexpr (MAPS && FRAME) {
-      const float a = fabsf(v);
-      if (i < g.fr[band][2] && j < g.fr[band][3])
-        out[item * g.maps_item + (int64_t)(g.fr[band][0] + i) * g.frame_w + g.fr[band][1] + j] = a;
-      mx = nan_max(mx, a);
-    } else {
-      put(g, off, numel, idx, v, mx);
     }
   }
 };
@@ -113,8 +96,7 @@ __device__ __forceinline__ float wave_max(float m) {
 // MC: 0 = one input plane per item; C > 0 = item is an image of C planes, averaged on load
 // CPL: level-1 output columns per lane (mw <= 64 * CPL): one wave covers a whole row
 // COOP: level 1 as a cooperative row stream (see phase 1 below) instead of wave-private chunks
-// FRAME (MAPS only): maps written in frame order on the mosaic canvas (PlaneGeom frame_w / fr)
-template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP, bool FRAME = false>
+template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP>
 __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))) k_plane_ana(const float* __restrict__ in, float* __restrict__ out,
                                                    float* __restrict__ band_max, const float* __restrict__ filt,
                                                    PlaneGeom g, WamNoise nz, int64_t n_items, int64_t S,
@@ -172,7 +154,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     if (tid < g.nbands) wg_max[tid] = 0u;
     __syncthreads();
   }
-  const BandOut<MAPS, FRAME> bo{out, item};
+  const BandOut<MAPS> bo{out, item};
   float* bufA = smem;
   float* bufB = smem + g.llcap;
 
@@ -313,11 +295,11 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
         const int i = i0 + h2;
         if (vcol && i < mh) {
           const int64_t idx = (int64_t)i * mw + vj;
-          if (lastlvl) bo.put(g, 0, g.off_a, bn, idx, i, vj, a, mx[3]);
+          if (lastlvl) bo.put(g, g.off_a, bn, idx, a, mx[3]);
           else bufA[idx] = a;
-          bo.put(g, g.band[0][0], g.off[0][0], bn, idx, i, vj, hh, mx[0]);
-          bo.put(g, g.band[0][1], g.off[0][1], bn, idx, i, vj, v, mx[1]);
-          bo.put(g, g.band[0][2], g.off[0][2], bn, idx, i, vj, d, mx[2]);
+          bo.put(g, g.off[0][0], bn, idx, hh, mx[0]);
+          bo.put(g, g.off[0][1], bn, idx, v, mx[1]);
+          bo.put(g, g.off[0][2], bn, idx, d, mx[2]);
         }
       }
     };
@@ -498,11 +480,11 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
         const int j = lane + 64 * c;
         if (j < mw && i >= i0 && i < i1) {  // a partial last group: rows outside the chunk
           const int64_t idx = (int64_t)i * mw + j;
-          if (lastlvl) bo.put(g, 0, g.off_a, bn, idx, i, j, av[c].x, mx[3]);
+          if (lastlvl) bo.put(g, g.off_a, bn, idx, av[c].x, mx[3]);
           else bufA[idx] = av[c].x;
-          bo.put(g, g.band[0][0], g.off[0][0], bn, idx, i, j, hd[c].x, mx[0]);
-          bo.put(g, g.band[0][1], g.off[0][1], bn, idx, i, j, av[c].y, mx[1]);
-          bo.put(g, g.band[0][2], g.off[0][2], bn, idx, i, j, hd[c].y, mx[2]);
+          bo.put(g, g.off[0][0], bn, idx, hd[c].x, mx[0]);
+          bo.put(g, g.off[0][1], bn, idx, av[c].y, mx[1]);
+          bo.put(g, g.off[0][2], bn, idx, hd[c].y, mx[2]);
         }
       }
     };
@@ -713,11 +695,11 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
                 vd = __builtin_elementwise_fma(fh2[k], f2{q.y, q.y}, vd);
               }
               const int64_t idx = (int64_t)i * mw + j;
-              if (lastlvl) bo.put(g, 0, g.off_a, bn, idx, i, j, ah.x, mx[3]);
+              if (lastlvl) bo.put(g, g.off_a, bn, idx, ah.x, mx[3]);
               else ldst[idx] = ah.x;
-              bo.put(g, g.band[l][0], g.off[l][0], bn, idx, i, j, ah.y, mx[0]);
-              bo.put(g, g.band[l][1], g.off[l][1], bn, idx, i, j, vd.x, mx[1]);
-              bo.put(g, g.band[l][2], g.off[l][2], bn, idx, i, j, vd.y, mx[2]);
+              bo.put(g, g.off[l][0], bn, idx, ah.y, mx[0]);
+              bo.put(g, g.off[l][1], bn, idx, vd.x, mx[1]);
+              bo.put(g, g.off[l][2], bn, idx, vd.y, mx[2]);
             }
           }
         }
@@ -937,11 +919,11 @@ PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items
   return g;
 }
 
-template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP, bool FRAME>
+template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP>
 int launch_plane_t(const PlaneGeom& g, int lds_bytes, int64_t n_items, const float* in, float* out, float* band_max,
                    const float* filt, const WamNoise& nz, int64_t S, int64_t group_items, const char* name,
                    double bytes, hipStream_t st) {
-  auto kern = k_plane_ana<L, CPL, NOISE, MC, MAPS, COOP, FRAME>;
+  auto kern = k_plane_ana<L, CPL, NOISE, MC, MAPS, COOP>;
   static std::atomic<uint64_t> attr_set{0};  // opt in to > 64 KB of dynamic LDS, once per device
   int dev = 0;
   WAM_HIP_CHECK(hipGetDevice(&dev));
@@ -958,7 +940,7 @@ int launch_plane_t(const PlaneGeom& g, int lds_bytes, int64_t n_items, const flo
   return WAM_OK;
 }
 
-template <bool NOISE, int MC, bool MAPS, bool FRAME = false>
+template <bool NOISE, int MC, bool MAPS>
 int dispatch_plane(const wam_plan* p, const PlaneGeom& g, int lds_bytes, int64_t n_items, const float* in,
                    float* out, float* band_max, const float* filt, const WamNoise& nz, int64_t S,
                    int64_t group_items, const char* name, double bytes, hipStream_t st) {
@@ -967,10 +949,10 @@ int dispatch_plane(const wam_plan* p, const PlaneGeom& g, int lds_bytes, int64_t
 #define WAM_PLANE_CASE(LL)                                                                                       \
   case LL:                                                                                                       \
     if (g.coop)                                                                                                  \
-      return two ? launch_plane_t<LL, 2, NOISE, MC, MAPS, true, FRAME>(WAM_PLANE_ARGS)                                  \
-                 : launch_plane_t<LL, 1, NOISE, MC, MAPS, true, FRAME>(WAM_PLANE_ARGS);                                 \
-    return two ? launch_plane_t<LL, 2, NOISE, MC, MAPS, false, FRAME>(WAM_PLANE_ARGS)                                   \
-               : launch_plane_t<LL, 1, NOISE, MC, MAPS, false, FRAME>(WAM_PLANE_ARGS);
+      return two ? launch_plane_t<LL, 2, NOISE, MC, MAPS, true>(WAM_PLANE_ARGS)                                  \
+                 : launch_plane_t<LL, 1, NOISE, MC, MAPS, true>(WAM_PLANE_ARGS);                                 \
+    return two ? launch_plane_t<LL, 2, NOISE, MC, MAPS, false>(WAM_PLANE_ARGS)                                   \
+               : launch_plane_t<LL, 1, NOISE, MC, MAPS, false>(WAM_PLANE_ARGS);
   switch (p->L) {
     WAM_PLANE_CASE(2) WAM_PLANE_CASE(4) WAM_PLANE_CASE(6) WAM_PLANE_CASE(8)
     default: return WAM_ERR_UNSUPPORTED;
@@ -1014,34 +996,16 @@ int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in
 }
 
 int launch_dwt2_plane_maps(const wam_plan* p, int64_t images, int channels, int64_t group_items, const float* grad,
-                           float* maps, float* band_max, hipStream_t st, int frame_h, int frame_w,
-                           const int32_t* rects) {
+                           float* maps, float* band_max, hipStream_t st) {
   if (((uintptr_t)grad & 15) || !dwt2_plane_supported(p, true)) return WAM_ERR_UNSUPPORTED;
   if (channels != 1 && channels != 3) return WAM_ERR_UNSUPPORTED;
   const int nh0 = (int)p->rec_shape[0], nw0 = (int)p->rec_shape[1];
   const float* filt = p->d_filt + WAM_F_ADJ_LO * p->L;
   PlaneGeom g = make_geom(p, nh0, nw0, WAM_MODE_ZERO, images);
-  double out_floats = (double)p->band_off[p->nbands];
-  if (rects) {  // frame-order maps (validated by the caller): one frame of pixels per item
-    if (p->nbands > 3 * WAM_MAX_LEVELS + 1) return WAM_ERR_UNSUPPORTED;
-    g.frame_w = frame_w;
-    g.maps_item = (int64_t)frame_h * frame_w;
-    for (int b = 0; b < p->nbands; ++b)
-      for (int k = 0; k < 4; ++k) g.fr[b][k] = rects[4 * b + k];
-    out_floats = 0;
-    for (int b = 0; b < p->nbands; ++b) out_floats += (double)rects[4 * b + 2] * rects[4 * b + 3];
-  }
   int rowlds, llcap;
   const int lds_bytes = lds_floats(p, nw0, rowlds, llcap) * 4;
   const WamNoise none{nullptr, 1, 1, 0, 0, 0, 0};
-  const double bytes = 4.0 * (double)images * ((double)channels * nh0 * nw0 + out_floats);
-  if (rects) {
-    if (channels == 3)
-      return dispatch_plane<false, 3, true, true>(p, g, lds_bytes, images, grad, maps, band_max, filt, none, 1,
-                                                  group_items, "k_plane_maps", bytes, st);
-    return dispatch_plane<false, 1, true, true>(p, g, lds_bytes, images, grad, maps, band_max, filt, none, 1,
-                                                group_items, "k_plane_maps", bytes, st);
-  }
+  const double bytes = 4.0 * (double)images * ((double)channels * nh0 * nw0 + (double)p->band_off[p->nbands]);
   if (channels == 3)
     return dispatch_plane<false, 3, true>(p, g, lds_bytes, images, grad, maps, band_max, filt, none, 1, group_items,
                                           "k_plane_maps", bytes, st);

@@ -527,35 +527,6 @@ int wam_waverec_adjoint_maps(const wam_plan* p, int64_t groups, int64_t group_it
   return WAM_OK;
 }
 
-int wam_waverec_adjoint_maps_frame(const wam_plan* p, int64_t groups, int64_t group_items, int channels,
-                                   const float* grad, int frame_h, int frame_w, const int32_t* rects, float* maps,
-                                   float* band_max, void* stream) {
-  if (!p || !p->d_filt || !grad || !maps || !band_max || !rects || groups < 0 || group_items < 0 || channels < 1 ||
-      frame_h < 1 || frame_w < 1)
-    return WAM_ERR_INVALID_ARG;
-  if ((int64_t)frame_h * frame_w >= (int64_t(1) << 31)) return WAM_ERR_INVALID_ARG;
-  if (!(wam_plan_caps(p) & WAM_CAP_ADJOINT_MAPS) || (channels != 1 && channels != 3) || p->ndim != 2)
-    return WAM_ERR_UNSUPPORTED;
-  // every band's visible part inside the frame and inside the band, no two bands on one pixel
-  for (int b = 0; b < p->nbands; ++b) {
-    const int32_t* r = rects + 4 * b;
-    if (r[0] < 0 || r[1] < 0 || r[2] < 0 || r[3] < 0 || r[2] > p->band_dims[b][0] || r[3] > p->band_dims[b][1] ||
-        (int64_t)r[0] + r[2] > frame_h || (int64_t)r[1] + r[3] > frame_w)
-      return WAM_ERR_INVALID_ARG;
-    for (int c = 0; c < b; ++c) {
-      const int32_t* q = rects + 4 * c;
-      if (r[2] && r[3] && q[2] && q[3] && r[0] < q[0] + q[2] && q[0] < r[0] + r[2] && r[1] < q[1] + q[3] &&
-          q[1] < r[1] + r[3])
-        return WAM_ERR_INVALID_ARG;
-    }
-  }
-  const int64_t images = groups * group_items;
-  if (images == 0) return WAM_OK;
-  if (!use_plane(p, true)) return WAM_ERR_UNSUPPORTED;
-  return launch_dwt2_plane_maps(p, images, channels, group_items, grad, maps, band_max, (hipStream_t)stream, frame_h,
-                                frame_w, rects);
-}
-
 int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha, int n_alpha, float* out,
                 void* ws, void* stream) {
   if (!p || !p->d_filt || !coeffs || !out || !ws || batch < 0 || n_alpha < 1) return WAM_ERR_INVALID_ARG;

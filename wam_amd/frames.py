@@ -121,46 +121,6 @@ def mosaic_map(plan, canvas_hw, base_hw, device):
     return _CACHE[key]
 
 
-def band_rects(plan, gmap, frame_hw):
-    """The mosaic map as per-band rectangles, for maps written in frame order
-    (wam_waverec_adjoint_maps_frame): ([nbands, 4] int32 host array of (frame row, frame column of
-    coefficient (0, 0), visible rows, visible columns), device src map p -> p (or -1 where no band
-    shows), the map's band table) -- or None when some band's visible coefficients are not the
-    top-left sub-rectangle of the band placed by a translation (then the coefficient-order path
-    runs). 2D plans only; cached per map."""
-    src, band = gmap
-    key = ("rects", plan, src.data_ptr(), band.data_ptr(), tuple(frame_hw))
-    if key not in _CACHE:
-        res = None
-        if plan.ndim == 2:
-            H, W = (int(v) for v in frame_hw)
-            s = src.cpu().numpy().reshape(H, W).astype(np.int64)
-            b = band.cpu().numpy().reshape(H, W).astype(np.int64)
-            rects = np.zeros((plan.nbands, 4), dtype=np.int32)
-            ok = True
-            for k in range(plan.nbands):
-                ys, xs = np.nonzero(b == k)
-                if ys.size == 0:
-                    continue
-                y0, x0, y1, x1 = ys.min(), xs.min(), ys.max() + 1, xs.max() + 1
-                bh, bw = (int(v) for v in plan.band_shapes[k])
-                if ys.size != (y1 - y0) * (x1 - x0) or y1 - y0 > bh or x1 - x0 > bw:
-                    ok = False
-                    break
-                ii, jj = np.meshgrid(np.arange(y1 - y0), np.arange(x1 - x0), indexing="ij")
-                if not np.array_equal(s[y0:y1, x0:x1], plan.band_offsets[k] + ii * bw + jj):
-                    ok = False
-                    break
-                rects[k] = (y0, x0, y1 - y0, x1 - x0)
-            if ok:
-                ident = torch.where(src >= 0, torch.arange(src.numel(), device=src.device, dtype=torch.int32),
-                                    torch.full_like(src, -1))
-                res = (rects, ident, band, gmap)  # gmap kept alive: its pointers are the key
-        _CACHE[key] = res
-    v = _CACHE[key]
-    return None if v is None else v[:3]
-
-
 def cube_map(plan, input_size, device):
     """BaseWAM3D.refactor (lib/wam_3D.py:127-166) as a gather map over item-major |g| maps.
     ``input_size`` is the refactor's cube size (the reference's self.input_size)."""

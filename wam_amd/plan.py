@@ -10,8 +10,6 @@ import torch
 from . import filters
 from ._lib import c_f32, c_i64, c_vp, check, lib, ptr, require_cuda, stream_of
 
-ERR_UNSUPPORTED = 3  # WAM_ERR_UNSUPPORTED (include/wam_hip.h)
-
 _CACHE = {}
 _LOCK = threading.Lock()
 PLAN_GENERIC = 1
@@ -155,25 +153,6 @@ class Plan:
                                            ptr(cg), ptr(ws), stream_of(dev)))
         return maps, bmax, cg
 
-    def adjoint_maps_frame(self, grad, groups, group_items, channels, frame_hw, rects):
-        """adjoint_maps with the maps written in frame order on the mosaic canvas (rects: host int32
-        [nbands, 4], frames.band_rects) -> (maps [images, H*W], band_max), or None when the fused
-        plane kernel does not take this plan / input (the caller then uses adjoint_maps)."""
-        require_cuda(grad, "grad")
-        grad = grad.contiguous()
-        images = groups * group_items
-        dev = grad.device
-        fh, fw = (int(v) for v in frame_hw)
-        maps = torch.empty(images * fh * fw, dtype=torch.float32, device=dev)
-        bmax = torch.zeros((groups, self.nbands), dtype=torch.float32, device=dev)
-        r = np.ascontiguousarray(rects, dtype=np.int32)
-        rc = lib.wam_waverec_adjoint_maps_frame(self._h, groups, group_items, channels, ptr(grad), fh, fw,
-                                                r.ctypes.data, ptr(maps), ptr(bmax), stream_of(dev))
-        if rc == ERR_UNSUPPORTED:
-            return None
-        check(rc)
-        return maps, bmax
-
 
 def get_plan(ndim, shape, levels, wavelet, mode, device, generic=False, flags=None):
     w = filters.get_wavelet(wavelet)
@@ -302,14 +281,6 @@ def frame_accumulate(groups, group_items, gmap, maps, maps_item_len, band_max, n
     check(lib.wam_frame_accumulate(groups, group_items, src.numel(), ptr(src), ptr(band), ptr(maps),
                                    maps_item_len, ptr(band_max), n_bands, int(bool(normalize)), ptr(frame),
                                    stream_of(frame.device)))
-
-
-def frame_accumulate_gather(groups, group_items, gmap, maps, maps_item_len, band_max, n_bands, normalize, frame):
-    """The per-pixel gather form (wam_frame_accumulate) with an explicit (src, band) map: used with
-    canvas-order maps (src[p] = p), where it reads each map contiguously."""
-    src, band = gmap
-    check(lib.wam_frame_accumulate(groups, group_items, src.numel(), ptr(src), ptr(band), ptr(maps), maps_item_len,
-                                   ptr(band_max), n_bands, int(bool(normalize)), ptr(frame), stream_of(frame.device)))
 
 
 def frame_trapz(groups, k0, group_items, gmap, maps, maps_item_len, band_max, n_bands, normalize, prev, acc,

@@ -35,8 +35,7 @@ from .profiling import phase
 from .constants import WaveletDetailTuple2d
 from .engine import (GradModel, LegacyNoise, Shard, auto_group, chunks, ig_weights, model_device, param_grad_sum,
                      require_gpu_device, wam_budget_bytes, wam_group)
-from .plan import (CAP_ADJOINT_MAPS, CAP_NOISY_WAVEDEC, disentangle_scales, frame_accumulate,
-                   frame_accumulate_gather, frame_trapz,
+from .plan import (CAP_ADJOINT_MAPS, CAP_NOISY_WAVEDEC, disentangle_scales, frame_accumulate, frame_trapz,
                    get_plan, item_sigma, noise_add, reproject_scales, subband_maps)
 
 
@@ -407,9 +406,6 @@ class WaveletAttribution2D(BaseWAM2D):
             legacy = LegacyNoise(sigma_all.cpu().numpy(), (c, h, w), self.random_seed, self.n_samples, dev)
         rec = plan.rec_shape
         last = None
-        # the mosaic as per-band rectangles: the fused maps kernel then writes each map straight onto
-        # the canvas and the accumulation reads it contiguously (None: coefficient-order maps)
-        rects = frames.band_rects(plan, gmap, (rh, rw))
         with param_grad_sum(self._grad.params(), shard):  # .grad as one process leaves it
             for s0, cnt in chunks(s_lo, s_hi, wgroup):
                 with phase("noise+wavedec2"):
@@ -427,22 +423,13 @@ class WaveletAttribution2D(BaseWAM2D):
                 with phase("model"):
                     g = self._gradients(img, y, cnt, n, group, batch)
                 with phase("adjoint+maps"):
-                    gv = g.view((cnt * n * c,) + rec)
-                    mf = None if rects is None else plan.adjoint_maps_frame(gv, cnt, n, c, (rh, rw), rects[0])
-                    if mf is None:
-                        maps, bmax, _ = self._adjoint_maps(plan, gv, cnt, n, c, full=False)
-                    else:
-                        maps, bmax = mf
+                    maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
                 if axis == "images":
                     with phase("all_reduce_max"):
                         shard.all_reduce_max(bmax)  # per-sample maxima over the whole batch (A.6)
                 with phase("accumulate"):
-                    if mf is None:
-                        frame_accumulate(cnt, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands,
-                                         self.normalize_coeffs, frame)
-                    else:  # canvas-order maps: src[p] = p, contiguous reads, same per-pixel sum order
-                        frame_accumulate_gather(cnt, n, (rects[1], rects[2]), maps, rh * rw, bmax, plan.nbands,
-                                                self.normalize_coeffs, frame)
+                    frame_accumulate(cnt, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs,
+                                     frame)
                 last = (plan, flat, None, cnt * n * c, (cnt - 1) * n, n, c)
                 last_g = g[(cnt - 1) * n:].reshape((n * c,) + rec)
         if legacy is not None:
