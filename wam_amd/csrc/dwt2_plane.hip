@@ -41,6 +41,12 @@ constexpr int kPlaneLdsCap = 160 * 1024 - 1024;
 #ifndef WAM_PLANE_SHARE
 #define WAM_PLANE_SHARE 1
 #endif
+// wave chunks at CPL = 2: lane l filters the ADJACENT columns 2l, 2l+1 (one run of L/2+1 LDS pairs
+// feeds both, and each band row is stored as float2 pairs) instead of columns l and l + 64;
+// WAM_PLANE_PAIRCOL=0 builds the split-column form for A/B
+#ifndef WAM_PLANE_PAIRCOL
+#define WAM_PLANE_PAIRCOL 1
+#endif
 
 struct PlaneGeom {
   int J;
@@ -66,6 +72,21 @@ template <bool MAPS>
 struct BandOut {
   float* out;
   int64_t item;
+  // columns idx, idx + 1 of one band row (pair: both inside the row) -- one 8-byte store (4-byte
+  // aligned rows: unaligned access mode) instead of two
+  __device__ __forceinline__ void put2(const PlaneGeom& g, int64_t off, int64_t numel, int64_t idx, float v0,
+                                       float v1, bool pair, float& mx) const {
+    typedef float f2s __attribute__((ext_vector_type(2)));
+    if constexpr (MAPS) {
+      put(g, off, numel, idx, v0, mx);
+      if (pair) put(g, off, numel, idx + 1, v1, mx);
+    } else if (pair) {
+      const f2s v = {v0, v1};
+      __builtin_memcpy(out + g.items_total * off + item * numel + idx, &v, 8);
+    } else {
+      out[g.items_total * off + item * numel + idx] = v0;
+    }
+  }
   __device__ __forceinline__ void put(const PlaneGeom& g, int64_t off, int64_t numel, int64_t idx, float v,
                                       float& mx) const {
     if constexpr (MAPS) {
@@ -402,10 +423,14 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     const bool end_share = SHARE && g.xend >= 0 && T >= 2 * (L - 2) && 2 * pe_rows + L - 2 >= 2 * (L - 2);
     const int T_stop = end_share ? T - HS : T;  // the loop's last step + 1
     float mx[4] = {0.f, 0.f, 0.f, 0.f};
+    // PAIRCOL: lane l owns columns 2l, 2l+1 (lanes past the row compute never-stored values from
+    // the in-bounds tail of their LDS row); else columns l, l + 64
+    constexpr bool PAIRCOL = WAM_PLANE_PAIRCOL && CPL == 2 && !MAPS;
+    auto colj = [&](int c) { return PAIRCOL ? 2 * lane + c : lane + 64 * c; };
     const float2* hsrc[CPL];
 #pragma unroll
     for (int c = 0; c < CPL; ++c)
-      hsrc[c] = reinterpret_cast<const float2*>(lds + kPadL + 2 * min(lane + 64 * c, mw - 1) - p);
+      hsrc[c] = reinterpret_cast<const float2*>(lds + kPadL + 2 * (PAIRCOL ? 2 * lane + c : min(colj(c), mw - 1)) - p);
 
     RowRegs<4, 1> f[NBL][NCH];
     int srow[NBL];
@@ -447,13 +472,29 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
       f2 acc[CPL];
 #pragma unroll
       for (int c = 0; c < CPL; ++c) acc[c] = f2{0.f, 0.f};
+      if constexpr (PAIRCOL) {
+        // column 2l+1's taps start one pair after column 2l's: L/2 + 1 pairs feed both
+        float2 xs[L / 2 + 1];
 #pragma unroll
-      for (int m2 = 0; m2 < L / 2; ++m2) {
+        for (int m2 = 0; m2 <= L / 2; ++m2) xs[m2] = hsrc[0][m2];
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          const float2 x = hsrc[c][m2];
-          acc[c] = __builtin_elementwise_fma(fh2[2 * m2], f2{x.x, x.x}, acc[c]);
-          acc[c] = __builtin_elementwise_fma(fh2[2 * m2 + 1], f2{x.y, x.y}, acc[c]);
+        for (int m2 = 0; m2 < L / 2; ++m2) {
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) {
+            const float2 x = xs[m2 + c];
+            acc[c] = __builtin_elementwise_fma(fh2[2 * m2], f2{x.x, x.x}, acc[c]);
+            acc[c] = __builtin_elementwise_fma(fh2[2 * m2 + 1], f2{x.y, x.y}, acc[c]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int m2 = 0; m2 < L / 2; ++m2) {
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) {
+            const float2 x = hsrc[c][m2];
+            acc[c] = __builtin_elementwise_fma(fh2[2 * m2], f2{x.x, x.x}, acc[c]);
+            acc[c] = __builtin_elementwise_fma(fh2[2 * m2 + 1], f2{x.y, x.y}, acc[c]);
+          }
         }
       }
 #pragma unroll
@@ -475,16 +516,33 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
           hd[c] = __builtin_elementwise_fma(f2{fh2[k].y, fh2[k].y}, r, hd[c]);  // (h, d) = sum fhi[k] * (lo, hi)
         }
       }
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        const int j = lane + 64 * c;
+      if constexpr (PAIRCOL) {
+        const int j = 2 * lane;
         if (j < mw && i >= i0 && i < i1) {  // a partial last group: rows outside the chunk
+          const bool pair = j + 1 < mw;
           const int64_t idx = (int64_t)i * mw + j;
-          if (lastlvl) bo.put(g, g.off_a, bn, idx, av[c].x, mx[3]);
-          else bufA[idx] = av[c].x;
-          bo.put(g, g.off[0][0], bn, idx, hd[c].x, mx[0]);
-          bo.put(g, g.off[0][1], bn, idx, av[c].y, mx[1]);
-          bo.put(g, g.off[0][2], bn, idx, hd[c].y, mx[2]);
+          if (lastlvl) {
+            bo.put2(g, g.off_a, bn, idx, av[0].x, av[1].x, pair, mx[3]);
+          } else {
+            bufA[idx] = av[0].x;
+            if (pair) bufA[idx + 1] = av[1].x;
+          }
+          bo.put2(g, g.off[0][0], bn, idx, hd[0].x, hd[1].x, pair, mx[0]);
+          bo.put2(g, g.off[0][1], bn, idx, av[0].y, av[1].y, pair, mx[1]);
+          bo.put2(g, g.off[0][2], bn, idx, hd[0].y, hd[1].y, pair, mx[2]);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+          const int j = lane + 64 * c;
+          if (j < mw && i >= i0 && i < i1) {  // a partial last group: rows outside the chunk
+            const int64_t idx = (int64_t)i * mw + j;
+            if (lastlvl) bo.put(g, g.off_a, bn, idx, av[c].x, mx[3]);
+            else bufA[idx] = av[c].x;
+            bo.put(g, g.off[0][0], bn, idx, hd[c].x, mx[0]);
+            bo.put(g, g.off[0][1], bn, idx, av[c].y, mx[1]);
+            bo.put(g, g.off[0][2], bn, idx, hd[c].y, mx[2]);
+          }
         }
       }
     };
@@ -588,7 +646,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
           for (int k = 0; k < HS; ++k)
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
-              const int j = lane + 64 * c;
+              const int j = colj(c);
               if (j < mw1) {
                 const f2 v = rv[c][(R0 + 2 * L - (L - 2) + k) % L];  // step T-(L-2)+k
                 xme[(2 * k) * mw1 + j] = v.x;
@@ -607,7 +665,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
           for (int k = HS - 1; k >= 0; --k) {  // partner's row k = this wave's step T-1-k
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
-              const int j = min(lane + 64 * c, mw1 - 1);  // lanes past the row: a duplicate, never stored
+              const int j = min(colj(c), mw1 - 1);  // lanes past the row: a duplicate, never stored
               rv[c][(R0 + 2 * L - 1 - k) % L] = f2{xpe[(2 * k) * mw1 + j], xpe[(2 * k + 1) * mw1 + j]};
             }
             if (k & 1) continue;  // step T-1-k is odd when k is even (T even)
