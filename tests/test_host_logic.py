@@ -1,6 +1,8 @@
 """Host-side logic of wam_amd on the CPU: mosaic / cube gather maps vs the reference's slice
 assignments, loss seed gradients vs autograd of diag(out[:, y]).mean(), the numpy noise stream,
 sample/step sharding and the sharded-accumulation weights."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -93,10 +95,32 @@ def test_seed_gradient_matches_autograd_of_reference_loss(y, n):
     (g_ref,) = torch.autograd.grad(loss, out)
     g, scale = engine.seed_gradient(out.detach(), y, groups, n)
     assert scale is None and torch.equal(g, g_ref)
-    # unit seed + fp32 scale (the bf16-model form): same gradient, the scale applied afterwards
+    # unit seed + fp32 scale (the bf16-model form): same gradient, the scale applied afterwards;
+    # a power-of-two scale is seeded directly (exact in bf16)
     gu, scale = engine.seed_gradient(out.detach(), y, groups, n, unit=True)
-    assert set(gu.unique().tolist()) <= {0.0, 1.0}
-    assert torch.equal(gu * scale, g_ref)
+    if scale is None:
+        assert torch.equal(gu, g_ref) and math.frexp(float(g_ref.abs().max()))[0] == 0.5
+    else:
+        assert set(gu.unique().tolist()) <= {0.0, 1.0}
+        assert torch.equal(gu * scale, g_ref)
+
+
+def test_bf16_power_of_two_seed_equals_unit_seed_then_scale():
+    """The bf16 backward seeded with a power-of-two loss scale gives the unit-seed gradient times
+    that scale bit for bit (rounding commutes with power-of-two scaling)."""
+    torch.manual_seed(3)
+    m = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.ReLU(), torch.nn.Flatten(),
+                            torch.nn.Linear(8 * 6 * 6, 10)).to(torch.bfloat16)
+    img = torch.randn(8, 3, 8, 8)
+    y = [1, 2, 3, 4, 5, 6, 7, 0]  # k = 8: scale 1/8
+    run = lambda t: m(t.to(torch.bfloat16))
+    g = engine.input_gradient(run, img, y, 1, 8)
+    x = img.detach().requires_grad_(True)
+    out = run(x)
+    seed = torch.zeros_like(out)
+    seed[torch.arange(8), torch.tensor(y)] = 1.0
+    (gu,) = torch.autograd.grad(out, x, grad_outputs=seed)
+    assert torch.equal(g, gu * 0.125)
 
 
 @pytest.mark.parametrize("y,n", [(3, 5), ([1, 5, 2, 2, 0], 5), ([4, 5], 5), (list(range(7)), 5)])

@@ -19,6 +19,7 @@ holds the single-process gradient.
 """
 import collections
 import contextlib
+import math
 
 import numpy as np
 import torch
@@ -51,7 +52,10 @@ def seed_gradient(out, y, groups, n, unit=False, batch=None):
     `total` items (a batch-sharded rank); the loss scale and y's indexing follow the whole batch.
     unit=True: the seed holds 1.0 where the loss gradient is non-zero and the loss scale (1/N^2,
     1/N or 1/k) is returned beside it, so a low-precision model output (bf16) does not round the
-    scale -- the caller applies it to the fp32 input gradient. Returns (seed, scale or None)."""
+    scale -- the caller applies it to the fp32 input gradient. A power-of-two scale (c2: 1/64) is
+    exact in bf16 and commutes with every rounding of the backward (absent under- / overflow), so
+    it is seeded directly (scale None): the same gradient without the caller's fp32 pass over it.
+    Returns (seed, scale or None)."""
     first, total = (0, n) if batch is None else batch
     go = torch.zeros_like(out, dtype=torch.float32)
     rows = torch.arange(groups * n, device=out.device)
@@ -67,7 +71,7 @@ def seed_gradient(out, y, groups, n, unit=False, batch=None):
         sel = torch.arange(n)[first + torch.arange(n) < k]       # local items with a diagonal entry
         rr = (torch.arange(groups)[:, None] * n + sel[None, :]).reshape(-1).to(out.device)
         cc = yy[first + sel].repeat(groups).to(out.device)
-    if unit:
+    if unit and math.frexp(float(val))[0] != 0.5:  # not a power of two
         go[rr, cc] = 1.0
         return go.to(out.dtype), float(val)
     go[rr, cc] = val.to(out.device)
