@@ -83,10 +83,13 @@ def trainable_params(model):
 
 
 def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=False, y_none_mean=False,
-                   input_dtype=None, batch=None, params=None):
-    """Gradient of the summed per-group reference losses w.r.t. img (fp32). params (default: the
-    model's parameters that require grad): their gradients are accumulated into .grad, as the
-    reference's loss.backward() does."""
+                   input_dtype=None, batch=None, params=None, out=None):
+    """Gradient of the summed per-group reference losses w.r.t. img (fp32, contiguous; written into
+    `out` when given). params (default: the model's parameters that require grad): their gradients
+    are accumulated into .grad, as the reference's loss.backward() does. The gradient is taken
+    w.r.t. the tensor the model is fed (bf16 and / or channels_last) and converted to img's dtype
+    and layout by ONE copy into the result -- autograd's cast and the layout copy were two more
+    passes over it; the values are the same (the bf16 -> fp32 cast is exact)."""
     img = img.detach().requires_grad_(True)
     inp = img if input_dtype is None else img.to(input_dtype)
     inp = inp.contiguous(memory_format=torch.channels_last) if channels_last and img.dim() == 4 else inp
@@ -94,27 +97,32 @@ def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=
     ctx = torch.autocast("cuda", dtype=autocast_dtype) if autocast_dtype is not None else contextlib.nullcontext()
     with torch.enable_grad():
         with ctx:
-            out = model(inp)
+            res = model(inp)
         # allow_unused: parameters outside the graph (an eval-mode auxiliary head, a conditional
         # branch) get no gradient, exactly as loss.backward() leaves their .grad untouched
         if y_none_mean:
             scale = None
-            gs = torch.autograd.grad(out.float().mean(), [img] + params, allow_unused=True)
+            gs = torch.autograd.grad(res.float().mean(), [inp] + params, allow_unused=True)
         else:
-            seed, scale = seed_gradient(out, y, groups, n, unit=out.dtype != torch.float32, batch=batch)
-            gs = torch.autograd.grad(out, [img] + params, grad_outputs=seed, allow_unused=True)
+            seed, scale = seed_gradient(res, y, groups, n, unit=res.dtype != torch.float32, batch=batch)
+            gs = torch.autograd.grad(res, [inp] + params, grad_outputs=seed, allow_unused=True)
     g = gs[0]
     if g is None:
         raise RuntimeError("the model's output does not depend on its input")
-    if scale is not None:
-        g = g * scale
     with torch.no_grad():
+        if out is None and g.dtype == img.dtype and g.is_contiguous():
+            out = g
+        else:
+            out = torch.empty(img.shape, dtype=img.dtype, device=img.device) if out is None else out
+            out.copy_(g)
+        if scale is not None:
+            out.mul_(scale)
         for p, gp in zip(params, gs[1:]):
             if gp is None:
                 continue
             gp = gp if scale is None else gp * scale
             _accumulate_param_grad(p, gp)
-    return g.contiguous()
+    return out
 
 
 # Parameter gradients of a sharded call (dist=True): while a `param_grad_sum` block is open the
@@ -197,13 +205,13 @@ class GradModel:
         """The parameters whose .grad a call accumulates (none for the folded copy)."""
         return [] if self.optimize else trainable_params(self.model)
 
-    def __call__(self, img, y, groups, n, y_none_mean=False, batch=None):
+    def __call__(self, img, y, groups, n, y_none_mean=False, batch=None, out=None):
         run = self._runner()
         if self.optimize:  # a folded copy: the user's parameters are not touched
             return input_gradient(run, img, y, groups, n, None, self.channels_last, y_none_mean,
-                                  input_dtype=self.autocast_dtype, batch=batch, params=[])
+                                  input_dtype=self.autocast_dtype, batch=batch, params=[], out=out)
         return input_gradient(run, img, y, groups, n, self.autocast_dtype, self.channels_last, y_none_mean,
-                              batch=batch)
+                              batch=batch, out=out)
 
 
 def legacy_noise(sigmas, item_shape, seed, samples, n_total=None):

@@ -355,7 +355,8 @@ class WaveletAttribution2D(BaseWAM2D):
             return self._grad(imgs, y, groups, n, batch=batch)
         out = torch.empty_like(imgs)
         for s0, cnt in chunks(0, groups, model_group):
-            out[s0 * n:(s0 + cnt) * n] = self._grad(imgs[s0 * n:(s0 + cnt) * n], y, cnt, n, batch=batch)
+            # each model group's gradient is written straight into its rows (one copy, no staging)
+            self._grad(imgs[s0 * n:(s0 + cnt) * n], y, cnt, n, batch=batch, out=out[s0 * n:(s0 + cnt) * n])
         return out
 
     @staticmethod
