@@ -52,6 +52,18 @@ import sys
 import tempfile
 import time
 
+# MIOpen picks the bf16 model's convolution solvers by timing them on a process's first use (about
+# a minute on a fresh box, and a noisy choice: some runs land 5 % slower). The bench
+# starts from the find database of an MI355X run instead (wam_amd/data/miopen: MIOpen's own
+# records, copied to a scratch directory it may update); a caller's MIOPEN_USER_DB_PATH wins.
+if "MIOPEN_USER_DB_PATH" not in os.environ:
+    _fdb = os.path.join(os.path.dirname(os.path.abspath(__file__)), "wam_amd", "data", "miopen")
+    if os.path.isdir(_fdb):
+        _udb = tempfile.mkdtemp(prefix="wam_miopen_")
+        for _f in os.listdir(_fdb):
+            shutil.copy(os.path.join(_fdb, _f), _udb)
+        os.environ["MIOPEN_USER_DB_PATH"] = _udb
+
 import numpy as np
 import torch
 import torch.distributed as dist
