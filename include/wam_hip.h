@@ -53,12 +53,12 @@ int wam_plan_create(wam_plan** plan, int ndim, const int64_t* shape, int levels,
 /* flags: WAM_PLAN_GENERIC forces the per-axis kernels, WAM_PLAN_NO_ROWS skips the row-resident
  * and plane-resident 2D kernels, WAM_PLAN_NO_PLANE skips only the plane-resident (all levels in
  * one workgroup) kernels; WAM_PLAN_NO_COOP / WAM_PLAN_FORCE_COOP pick the plane kernels' level-1
- * form (wave chunks / cooperative row stream) and WAM_PLAN_LINE selects the line-streaming SmoothGrad
- * analysis (one wave per plane, all levels streamed) instead of the size-based choice (all used by tests
- * to cross-check the fused 2D kernels); 0 selects the fastest path.
+ * form (wave chunks / cooperative row stream) instead of the size-based choice (all used by tests to
+ * cross-check the fused 2D kernels); 0 selects the fastest path. Bit 32 (a line-streaming analysis
+ * that never beat the plane kernel) is retired and ignored.
  * wam_plan_create == wam_plan_create_ex(..., 0). */
 enum wam_plan_flags { WAM_PLAN_GENERIC = 1, WAM_PLAN_NO_ROWS = 2, WAM_PLAN_NO_PLANE = 4, WAM_PLAN_NO_COOP = 8,
-                      WAM_PLAN_FORCE_COOP = 16, WAM_PLAN_LINE = 32 };
+                      WAM_PLAN_FORCE_COOP = 16 };
 int wam_plan_create_ex(wam_plan** plan, int ndim, const int64_t* shape, int levels,
                        const double* dec_lo, const double* dec_hi,
                        const double* rec_lo, const double* rec_hi, int filt_len, int mode, int flags);

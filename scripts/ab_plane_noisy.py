@@ -1,9 +1,8 @@
-"""A/B of the c2 SmoothGrad analysis: line-streaming kernel (plan flag WAM_PLAN_LINE = 32) vs the
-plane-resident kernel (flags 0) at several sample counts (4,800 planes = c2; 4,032 = one round of 4 waves
-per SIMD), timed with the library's HIP events. WAM_LIB_PATH selects a variant build
-(scripts/build_variants.py).
+"""A/B of the c2 SmoothGrad analysis (`k_plane_ana<noise>`) at several sample counts (4,800 planes =
+c2; 4,032 = one round of 4 waves per SIMD) and plan flags (0; 8 = NO_COOP; 16 = FORCE_COOP), timed with
+the library's HIP events. WAM_LIB_PATH selects a variant build (scripts/build_variants.py).
 
-usage: python scripts/ab_line.py [--iters 20] [--samples 25,21] [--flags 0,32]
+usage: python scripts/ab_plane_noisy.py [--iters 20] [--samples 25,21] [--flags 0]
 """
 import argparse
 import os
@@ -21,7 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--samples", default="25,21")
-    ap.add_argument("--flags", default="0,32")
+    ap.add_argument("--flags", default="0")
     ap.add_argument("--wavelet", default="db4")
     ap.add_argument("--J", type=int, default=3)
     args = ap.parse_args()

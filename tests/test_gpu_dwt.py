@@ -442,41 +442,6 @@ def test_plane_coop_equals_wave_chunks(wam, wav, shape, J, mode):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("wav,shape,J,mode", [("db4", (224, 224), 3, "reflect"), ("haar", (224, 224), 3, "reflect"),
-                                              ("db2", (64, 96), 3, "symmetric"), ("db3", (100, 84), 2, "zero"),
-                                              ("db4", (37, 52), 2, "reflect"), ("db4", (224, 224), 1, "constant"),
-                                              ("sym4", (36, 200), 3, "constant"), ("db4", (17, 16), 3, "reflect"),
-                                              ("db4", (224, 224), 2, "periodic"), ("coif1", (61, 124), 3, "zero")])
-def test_line_stream_equals_plane_kernel(wam, wav, shape, J, mode):
-    """Line-streaming SmoothGrad analysis (one wave per plane, levels 2..J streamed through LDS
-    rings indexed by source row; plan flag WAM_PLAN_LINE) vs the plane-resident kernel: the same
-    taps in the same fma order, so bit-identical; the line kernel must be the one that ran."""
-    from wam_amd import plan as P
-    line = wam.get_plan(2, shape, J, wav, mode, "cuda", flags=P.PLAN_LINE)
-    ref = wam.get_plan(2, shape, J, wav, mode, "cuda")
-    if not (line.caps & wam.CAP_NOISY_WAVEDEC and ref.caps & wam.CAP_NOISY_WAVEDEC):
-        pytest.skip("no fused noisy analysis for this geometry")
-    torch.manual_seed(17)
-    N, C, S = 3, 3, 5
-    x = torch.randn((N, C) + shape, device="cuda")
-    sigma = wam.item_sigma(x, C * shape[0] * shape[1], C * shape[0] * shape[1], 0.3)
-    torch.cuda.synchronize()
-    P.timing_drain()
-    P.timing_enable(True)
-    a = line.wavedec_noisy(x, sigma, S, N, C, seed=21, sample_base=3)
-    torch.cuda.synchronize()
-    P.timing_enable(False)
-    names = {r[0] for r in P.timing_drain()}
-    b = ref.wavedec_noisy(x, sigma, S, N, C, seed=21, sample_base=3)
-    assert torch.equal(a, b)
-    noisy = wam.noise_add(x, sigma, S, N, C * shape[0] * shape[1], C * shape[0] * shape[1], seed=21, sample_base=3)
-    gen = wam.get_plan(2, shape, J, wav, mode, "cuda", generic=True)
-    c = gen.wavedec(noisy.view((S * N * C,) + shape))
-    assert float((a - c).abs().max()) <= 1e-5 * float(c.abs().max())
-    if shape[1] % 4 == 0 and J <= 3 and mode != "periodic" and max(shape) <= 224:
-        assert "k_plane_line<noise>" in names, names
-
-
 @pytest.mark.parametrize("items,stride,length", [(64, 3 * 224 * 224, 3 * 224 * 224), (256, 80000, 80000),
                                                  (16, 128 ** 3, 128 ** 3), (3, 1001, 999), (5, 4096, 4096),
                                                  (1, 7, 7), (2, 40000, 37)])

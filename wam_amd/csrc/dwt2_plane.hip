@@ -36,17 +36,9 @@ constexpr int kPT = 64 * kPW;          // threads per workgroup
 constexpr int kPlaneMaxW = 256;        // level-0 row width (one float4 per lane)
 constexpr int kPlaneMaxMW = 128;       // level-1 output width (two columns per lane)
 constexpr int kPlaneLdsCap = 160 * 1024 - 1024;
-// noisy wave-chunk level 1 with the halo rows of the boundaries where a pair of waves starts
-// computed once (bidirectional chunks); WAM_PLANE_SHARE=0 builds the one-direction form for A/B
-#ifndef WAM_PLANE_SHARE
-#define WAM_PLANE_SHARE 1
-#endif
-// wave chunks at CPL = 2: lane l filters the ADJACENT columns 2l, 2l+1 (one run of L/2+1 LDS pairs
-// feeds both, and each band row is stored as float2 pairs) instead of columns l and l + 64;
-// WAM_PLANE_PAIRCOL=0 builds the split-column form for A/B
-#ifndef WAM_PLANE_PAIRCOL
-#define WAM_PLANE_PAIRCOL 1
-#endif
+// noisy wave-chunk level 1 computes the halo rows of the boundaries where a pair of waves meets
+// once (bidirectional chunks); at CPL = 2 lane l filters the ADJACENT columns
+// 2l, 2l+1 (one run of L/2+1 LDS pairs feeds both, each band row stored as float2 pairs)
 
 struct PlaneGeom {
   int J;
@@ -408,7 +400,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     // the LL_1 area of LDS (empty until the first emit), instead of both computing all six -- a
     // quarter of the halo rows (each row is fetched, noised and filtered once per wave that needs
     // it). Local step s runs 0 .. T-1 over the wave's ext rows in its own direction; ring slot s % L.
-    constexpr bool SHARE = WAM_PLANE_SHARE && NOISE && MC == 0 && L >= 4 && NBL == 2;
+    constexpr bool SHARE = NOISE && MC == 0 && L >= 4 && NBL == 2;
     constexpr int HS = (L - 2) / 2;  // shared rows computed by each wave of a pair
     const bool up = SHARE && !(wv & 1);
     const int pw = wv ^ 1;  // partner
@@ -425,7 +417,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     float mx[4] = {0.f, 0.f, 0.f, 0.f};
     // PAIRCOL: lane l owns columns 2l, 2l+1 (lanes past the row compute never-stored values from
     // the in-bounds tail of their LDS row); else columns l, l + 64
-    constexpr bool PAIRCOL = WAM_PLANE_PAIRCOL && CPL == 2 && !MAPS;
+    constexpr bool PAIRCOL = CPL == 2 && !MAPS;
     auto colj = [&](int c) { return PAIRCOL ? 2 * lane + c : lane + 64 * c; };
     const float2* hsrc[CPL];
 #pragma unroll
@@ -926,7 +918,7 @@ int lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap, bool noisy =
     if (ll2 > bcap) bcap = ll2;
   }
   if (xend) *xend = -1;
-  if (noisy && WAM_PLANE_SHARE) {
+  if (noisy) {
     // the END-boundary exchange behind the wave rows: (kPW/2 - 1) boundaries x 2 directions x
     // (L-2)/2 rows x (lo, hi) x mw floats, if two workgroups still fit a CU
     const int64_t xe = (int64_t)(kPW / 2 - 1) * 2 * (p->L - 2) * p->lout[0][1];
@@ -1040,8 +1032,6 @@ int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in
   const double in_planes = nz ? (double)nz->images * nz->channels : (double)items;
   const double bytes = 4.0 * (in_planes * nh0 * nw0 + (double)items * p->band_off[p->nbands]);
   if (nz) {
-    const int rc = launch_dwt2_line_analysis(p, items, in, coeffs, nz, n_samples, st);
-    if (rc != WAM_ERR_UNSUPPORTED) return rc;
     if (items != n_samples * nz->images * nz->channels) return WAM_ERR_INVALID_ARG;
     // the fused noise counts element groups of an image in 32 bits (wam_normal4_x2)
     if ((int64_t)nz->channels * nh0 * nw0 >= (int64_t(1) << 34)) return WAM_ERR_UNSUPPORTED;

@@ -67,10 +67,6 @@ int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in
                                const WamNoise* nz, int64_t n_samples, hipStream_t st);
 int launch_dwt2_plane_maps(const wam_plan* p, int64_t images, int channels, int64_t group_items, const float* grad,
                            float* maps, float* band_max, hipStream_t st);
-// line-streaming SmoothGrad analysis (dwt2_line.hip): one wave per plane, all levels streamed
-bool dwt2_line_supported(const wam_plan* p, bool adjoint);
-int launch_dwt2_line_analysis(const wam_plan* p, int64_t items, const float* in, float* coeffs, const WamNoise* nz,
-                              int64_t n_samples, hipStream_t st);
 bool dwt2_plane_syn_supported(const wam_plan* p);
 int launch_dwt2_plane_synthesis(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha,
                                 int n_alpha, float* out, hipStream_t st);

@@ -173,7 +173,6 @@ PLAN_NO_ROWS = 2
 PLAN_NO_PLANE = 4
 PLAN_NO_COOP = 8
 PLAN_FORCE_COOP = 16
-PLAN_LINE = 32
 CAP_NOISY_WAVEDEC = 1
 CAP_ADJOINT_MAPS = 2
 
