@@ -65,49 +65,87 @@ class AmplitudeToDB(torch.nn.Module):
 
 # ---------------------------------------------------------------------------- librosa mel inversion
 def slaney_mel_basis(sr, n_fft, n_mels):
-    """librosa.filters.mel(sr=sr, n_fft=n_fft, n_mels=n_mels) with its defaults (htk=False:
-    Slaney scale, linear below 1 kHz at 200/3 Hz per mel, logarithmic above with step
-    ln(6.4)/27; fmin 0, fmax sr/2; norm='slaney'), float64, element by element."""
+    """librosa.filters.mel(sr=sr, n_fft=n_fft, n_mels=n_mels, dtype=float32) with its defaults
+    (htk=False: Slaney scale, linear below 1 kHz at 200/3 Hz per mel, logarithmic above with step
+    ln(6.4)/27; fmin 0, fmax sr/2; norm='slaney'), element by element in librosa's rounding order:
+    bin frequencies j * (1 / (n_fft * (1 / sr))) (np.fft.rfftfreq), mel points by np.linspace, each
+    triangle value rounded to float32, then multiplied by the float64 area norm 2 / (f[i+2] - f[i])
+    and rounded again."""
     import numpy as np
 
     def hz2mel(f):
-        return f / (200.0 / 3) if f < 1000.0 else 15.0 + math.log(f / 1000.0) / (math.log(6.4) / 27.0)
+        return f / (200.0 / 3) if f < 1000.0 else 1000.0 / (200.0 / 3) + math.log(f / 1000.0) / (math.log(6.4) / 27.0)
 
     def mel2hz(m):
-        return (200.0 / 3) * m if m < 15.0 else 1000.0 * math.exp((math.log(6.4) / 27.0) * (m - 15.0))
+        return (200.0 / 3) * m if m < 1000.0 / (200.0 / 3) else 1000.0 * math.exp((math.log(6.4) / 27.0) * (m - 1000.0 / (200.0 / 3)))
 
     n_f = 1 + n_fft // 2
-    freqs = [i * (sr / 2.0) / (n_f - 1) for i in range(n_f)]
-    lo, hi = hz2mel(0.0), hz2mel(sr / 2.0)
-    pts = [mel2hz(lo + (hi - lo) * k / (n_mels + 1)) for k in range(n_mels + 2)]
-    w = np.zeros((n_mels, n_f))
+    step = 1.0 / (n_fft * (1.0 / sr))
+    freqs = [j * step for j in range(n_f)]
+    pts = [mel2hz(float(m)) for m in np.linspace(hz2mel(0.0), hz2mel(float(sr) / 2), n_mels + 2)]
+    w = np.zeros((n_mels, n_f), dtype=np.float32)
     for i in range(n_mels):
+        norm = 2.0 / (pts[i + 2] - pts[i])
         for j, f in enumerate(freqs):
-            lower = (f - pts[i]) / (pts[i + 1] - pts[i])
+            lower = -(pts[i] - f) / (pts[i + 1] - pts[i])
             upper = (pts[i + 2] - f) / (pts[i + 2] - pts[i + 1])
-            w[i, j] = max(0.0, min(lower, upper)) * 2.0 / (pts[i + 2] - pts[i])
+            w[i, j] = np.float32(float(np.float32(max(0.0, min(lower, upper)))) * norm)
     return w
+
+
+MAX_MEM_BLOCK = 2 ** 8 * 2 ** 10  # librosa.util.MAX_MEM_BLOCK
+
+
+def _nnls_obj(x, shape, A, B):
+    """librosa.util._nnls._nnls_obj: float64 objective / gradient of a float32 basis and data."""
+    import numpy as np
+    x = x.reshape(shape)
+    diff = A.astype(np.float64) @ x - B
+    return (1 / B.size) * 0.5 * np.sum(diff ** 2), ((1 / B.size) * (A.astype(np.float64).T @ diff)).ravel()
+
+
+def _nnls_lbfgs_block(A, B, x_init):
+    import scipy.optimize
+    shape = x_init.shape
+    x, _, _ = scipy.optimize.fmin_l_bfgs_b(_nnls_obj, x_init, args=(shape, A, B), bounds=[(0, None)] * x_init.size,
+                                           m=A.shape[1])
+    return x.reshape(shape)
+
+
+def nnls(A, B):
+    """librosa.util.nnls(A, B) for a 2D float32 B [M, T]: x_init = clip(pinv(A) @ B, 0) in float32;
+    scipy L-BFGS-B (bounds x >= 0, history m = A.shape[1], scipy's default tolerances) on
+    0.5 / B.size * ||A x - B||^2 over all columns if they fit MAX_MEM_BLOCK bytes, else per block of
+    columns (each block from its own columns of x_init); result in A's dtype."""
+    import numpy as np
+    n_columns = max(int(MAX_MEM_BLOCK // (B.shape[0] * A.itemsize)), 1)
+    x_init = np.linalg.pinv(A) @ B
+    np.clip(x_init, 0, None, out=x_init)
+    if B.shape[-1] <= n_columns:
+        return _nnls_lbfgs_block(A, B, x_init).astype(A.dtype)
+    x = x_init.copy()
+    for s in range(0, B.shape[-1], n_columns):
+        t = min(s + n_columns, B.shape[-1])
+        x[:, s:t] = _nnls_lbfgs_block(A, B[:, s:t], x_init[:, s:t])
+    return x
 
 
 def mel_to_stft(M, sr, n_fft, power=2.0):
     """librosa.feature.inverse.mel_to_stft (librosa's published algorithm; librosa is absent
-    offline): A = the float32 mel basis; nnls(A, M): x0 = lstsq(A, M) clipped at 0, then scipy
-    L-BFGS-B on 0.5 / M.size * ||A x - M||^2 with bounds x >= 0 and history m = A.shape[1]
-    (one block: the columns fit librosa's 256 KiB block); x ** (1 / power). M [n_mels, T]."""
+    offline): A = the float32 mel basis of M's dtype, nnls(A, M), then x ** (1 / power) in float32.
+    M [n_mels, T] float32."""
     import numpy as np
-    import scipy.optimize
-    A = slaney_mel_basis(sr, n_fft, M.shape[0]).astype(np.float32)
     B = np.asarray(M, dtype=np.float32)
-    x0 = np.linalg.lstsq(A, B, rcond=None)[0]
-    np.clip(x0, 0, None, out=x0)
-    shape = x0.shape
+    A = slaney_mel_basis(sr, n_fft, B.shape[0])
+    x = nnls(A, B)
+    return np.power(x, 1.0 / power, out=x), A
 
-    def obj(x):
-        x = x.reshape(shape)
-        diff = A @ x - B
-        return (0.5 / B.size) * np.sum(diff ** 2), ((1.0 / B.size) * (A.T @ diff)).ravel()
-    x, _, _ = scipy.optimize.fmin_l_bfgs_b(obj, x0.ravel(), bounds=[(0, None)] * x0.size, m=A.shape[1])
-    return np.power(x.reshape(shape).astype(np.float32), 1.0 / power), A
+
+def process_in_chunks(melspec, chunk_size, sr, n_fft):
+    """lib/wam_1D.py:442-448: mel_to_stft per chunk of chunk_size frames, hstacked."""
+    import numpy as np
+    return np.hstack([mel_to_stft(melspec[:, i:i + chunk_size], sr, n_fft)[0]
+                      for i in range(0, melspec.shape[1], chunk_size)])
 
 
 def nnls_exact(A, B):

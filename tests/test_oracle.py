@@ -141,7 +141,8 @@ def test_slaney_mel_basis_restatements_agree():
     for sr, n_fft, n_mels in [(16000, 256, 32), (44100, 1024, 128), (22050, 2048, 64)]:
         a, b = om.slaney_mel_basis(sr, n_fft, n_mels), wm.slaney_mel_basis(sr, n_fft, n_mels)
         assert a.shape == b.shape == (n_mels, 1 + n_fft // 2)
-        assert np.abs(a - b).max() <= 1e-6 * np.abs(a).max()
+        # both restate librosa's rounding sequence (float32 triangle, then the float64 area norm)
+        assert a.dtype == b.dtype == np.float32 and np.array_equal(a, b)
         assert (a >= 0).all() and (a.max(axis=1) > 0).all()
     assert abs(wm._slaney_hz_to_mel(1000.0) - 15.0) < 1e-12 and abs(wm._slaney_hz_to_mel(500.0) - 7.5) < 1e-12
     assert abs(wm._slaney_mel_to_hz(wm._slaney_hz_to_mel(6400.0)) - 6400.0) < 1e-9
@@ -153,7 +154,42 @@ def test_librosa_lbfgs_restatement_is_feasible_and_not_better_than_exact_nnls():
     fb = om.melscale_fbanks(129, 0.0, 8000.0, 32, 16000).numpy()
     B = (fb.T @ (rs.standard_normal((129, 12)) ** 2 * 50)).astype(np.float32)
     S, A = om.mel_to_stft(B, 16000, 256)
-    assert S.shape == (129, 12) and (S >= 0).all()
+    assert S.shape == (129, 12) and S.dtype == np.float32 and (S >= 0).all()
     xe = om.nnls_exact(A, B)
     f = lambda x: 0.5 * np.sum((A.astype(np.float64) @ x - B) ** 2)  # noqa: E731
     assert f(xe) <= f(S.astype(np.float64) ** 2) * (1 + 1e-9)
+
+
+@pytest.mark.parametrize("n_mels,T,chunk", [(32, 24, 7), (128, 40, 100), (256, 300, 300)])
+def test_product_lbfgsb_driver_matches_librosa_restatement(n_mels, T, chunk):
+    """The product's host side of compute_spectrogram (wam_amd.melspec: block split by librosa's
+    MAX_MEM_BLOCK, scipy L-BFGS-B with m = F from the clipped pinv start) fed the oracle's float64
+    objective gives the oracle's librosa restatement (to 1e-6 of the largest magnitude: LAPACK's
+    float32 SVD inside np.linalg.pinv is not bit-reproducible across the two equal bases' memory
+    alignment, and L-BFGS-B carries a 1e-14 change of its start into ~1e-8 of its result); (256, 300)
+    exercises librosa's multi-block branch (256 columns per block at n_mels = 256)."""
+    from oracle import melspec as om
+    from wam_amd import melspec as wm
+    sr, n_fft = 16000, 512
+    rs = np.random.RandomState(n_mels)
+    fb = om.melscale_fbanks(n_fft // 2 + 1, 0.0, sr / 2, n_mels, sr).numpy()
+    mel = (fb.T @ (rs.standard_normal((n_fft // 2 + 1, T)) ** 2 * 40)).astype(np.float32)
+    A = wm.slaney_mel_basis(sr, n_fft, n_mels)
+    pinv = np.linalg.pinv(A)
+    got = []
+    for i in range(0, T, chunk):
+        B = mel[:, i:i + chunk]
+        ncol = wm.lbfgsb_columns(B.shape[0])
+        x_init = np.clip(pinv @ B, 0, None)
+        x = x_init.copy()
+        for s in range(0, B.shape[1], ncol):
+            t = min(s + ncol, B.shape[1])
+            Bb = B[:, s:t]
+            x[:, s:t] = wm.nnls_lbfgsb_block(lambda v, Bb=Bb: om._nnls_obj(v, (A.shape[1], t - s), A, Bb),
+                                             x_init[:, s:t], A.shape[1]).astype(np.float32)
+        got.append(np.power(x, 0.5))
+    got = np.hstack(got)
+    ref = om.process_in_chunks(mel, chunk, sr, n_fft)
+    assert (n_mels != 256) or wm.lbfgsb_columns(256) == 256 < T
+    assert got.shape == ref.shape == (n_fft // 2 + 1, T) and got.dtype == ref.dtype == np.float32
+    assert np.abs(got - ref).max() <= 1e-6 * np.abs(ref).max()

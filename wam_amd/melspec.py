@@ -164,36 +164,44 @@ def _slaney_mel_to_hz(m):
 
 
 def slaney_mel_basis(sample_rate, n_fft, n_mels):
-    """librosa.filters.mel(sr, n_fft, n_mels) defaults (the basis librosa.feature.inverse.mel_to_stft
-    inverts, lib/wam_1D.py:446): Slaney mel scale (htk=False), fmin 0, fmax sr / 2, triangles over
-    the rfft bin frequencies, 'slaney' area normalisation 2 / (f[i+2] - f[i]); float32 [n_mels,
-    1 + n_fft // 2]. Published algorithm of librosa (absent offline: parity unpinned)."""
-    fftfreqs = np.linspace(0.0, sample_rate / 2.0, 1 + n_fft // 2)
-    mel_f = _slaney_mel_to_hz(np.linspace(_slaney_hz_to_mel(0.0), _slaney_hz_to_mel(sample_rate / 2.0), n_mels + 2))
+    """librosa.filters.mel(sr, n_fft, n_mels, dtype=float32) defaults (the basis
+    librosa.feature.inverse.mel_to_stft inverts, lib/wam_1D.py:446): Slaney mel scale (htk=False),
+    fmin 0, fmax sr / 2, triangles over the rfft bin frequencies (np.fft.rfftfreq), each triangle
+    rounded to float32 and then scaled by the 'slaney' area norm 2 / (f[i+2] - f[i]) in float64 and
+    rounded again -- librosa's own rounding sequence. [n_mels, 1 + n_fft // 2] float32.
+    Published algorithm of librosa (absent offline: parity unpinned)."""
+    fftfreqs = np.arange(0, 1 + n_fft // 2) * (1.0 / (n_fft * (1.0 / sample_rate)))
+    mel_f = _slaney_mel_to_hz(np.linspace(_slaney_hz_to_mel(0.0), _slaney_hz_to_mel(float(sample_rate) / 2),
+                                          n_mels + 2))
     fdiff = np.diff(mel_f)
     ramps = np.subtract.outer(mel_f, fftfreqs)
-    w = np.zeros((n_mels, 1 + n_fft // 2))
+    w = np.zeros((n_mels, 1 + n_fft // 2), dtype=np.float32)
     for i in range(n_mels):
         lower = -ramps[i] / fdiff[i]
         upper = ramps[i + 2] / fdiff[i + 1]
         w[i] = np.maximum(0, np.minimum(lower, upper))
-    w *= (2.0 / (mel_f[2:n_mels + 2] - mel_f[:n_mels]))[:, None]
-    return w.astype(np.float32)
+    w *= (2.0 / (mel_f[2:n_mels + 2] - mel_f[:n_mels]))[:, np.newaxis]
+    return w
 
 
 class MelInverse:
-    """Device data of the NNLS mel inversion for one (sr, n_fft, n_mels): the basis A [M, F], its
-    Gram matrix A^T A [F, F], A^T, the minimum-norm least-squares operator pinv(A) [F, M] (librosa's
-    initial point) and the Lipschitz constant ||A||_2^2 of the gradient (float64 SVD on the host)."""
+    """Device data of the NNLS mel inversion for one (sr, n_fft, n_mels): the float32 basis A [M, F]
+    and A^T; the basis widened to float64 (A64, A64^T: librosa's objective multiplies the float32
+    basis into float64 iterates); pinv(A) [F, M] computed as librosa does (np.linalg.pinv of the
+    float32 basis, i.e. a float32 SVD: librosa's initial point); for the exact solver the Gram
+    matrix A^T A and the Lipschitz constant ||A||_2^2 (float64 on the host)."""
 
     def __init__(self, sample_rate, n_fft, n_mels, device):
         A = slaney_mel_basis(sample_rate, n_fft, n_mels)
         A64 = A.astype(np.float64)
+        self.n_mels = n_mels
         self.lip = float(np.linalg.norm(A64, 2) ** 2)
         self.A = torch.tensor(A, device=device)
         self.At = self.A.t().contiguous()
+        self.A64 = torch.tensor(A64, device=device)
+        self.A64t = self.A64.t().contiguous()
         self.G = torch.tensor((A64.T @ A64).astype(np.float32), device=device)
-        self.pinv = torch.tensor(np.linalg.pinv(A64).astype(np.float32), device=device)
+        self.pinv = torch.tensor(np.linalg.pinv(A), device=device)
 
     @staticmethod
     def get(sample_rate, n_fft, n_mels, device):
@@ -203,8 +211,81 @@ class MelInverse:
         return _MELINV[key]
 
 
+# librosa.util.MAX_MEM_BLOCK: librosa's nnls solves at most this many bytes of columns per L-BFGS-B run
+MAX_MEM_BLOCK = 2 ** 8 * 2 ** 10
+
+
+def lbfgsb_columns(n_mels, itemsize=4):
+    """Columns per L-BFGS-B block in librosa.util.nnls for a [n_mels, T] float32 right-hand side."""
+    return max(1, int(MAX_MEM_BLOCK // (n_mels * itemsize)))
+
+
+def nnls_lbfgsb_block(evaluate, x0, m):
+    """One librosa ``_nnls_lbfgs_block``: scipy.optimize.fmin_l_bfgs_b with bounds x >= 0 and history
+    m = A.shape[1] from x0 (float32 [F, T], already clipped), scipy's default tolerances (factr 1e7,
+    pgtol 1e-5, 15,000 iterations / evaluations). evaluate(x float64 flat) -> (value, gradient flat)
+    is the objective 0.5 / B.size * ||A x - B||^2. Host logic only; returns float64 [F, T]."""
+    import scipy.optimize
+    shape = tuple(x0.shape)
+    xi = np.asarray(x0)
+    x, _, _ = scipy.optimize.fmin_l_bfgs_b(evaluate, xi, bounds=[(0, None)] * xi.size, m=m)
+    return x.reshape(shape)
+
+
+def device_objective(inv, B):
+    """librosa's ``_nnls_obj`` for one block on the device in float64: diff = A x - B (the float32
+    basis and right-hand side widened, as numpy's einsum widens them against the float64 iterate),
+    value = (1 / B.size) * 0.5 * sum(diff^2), gradient = (1 / B.size) * A^T diff. The iterate goes
+    host -> device and (value, gradient) device -> host once per evaluation through pinned buffers
+    (scipy's L-BFGS-B drives the iteration on the host, as in the reference)."""
+    F, T = inv.A.shape[1], B.shape[1]
+    dev = B.device
+    B64 = B.to(torch.float64)
+    scale = 1.0 / B.numel()
+    xh = torch.empty(F * T, dtype=torch.float64, pin_memory=True)
+    oh = torch.empty(F * T + 1, dtype=torch.float64, pin_memory=True)
+    xd = torch.empty((F, T), dtype=torch.float64, device=dev)
+    od = torch.empty(F * T + 1, dtype=torch.float64, device=dev)
+    xh_np, oh_np = xh.numpy(), oh.numpy()
+
+    def evaluate(x):
+        xh_np[:] = x
+        xd.view(-1).copy_(xh, non_blocking=True)
+        diff = torch.addmm(B64, inv.A64, xd, alpha=1.0, beta=-1.0)          # A x - B
+        torch.sum(diff * diff, out=od[:1].view(()))
+        od[:1].mul_(scale * 0.5)
+        torch.mm(inv.A64t, diff, out=od[1:].view(F, T))
+        od[1:].mul_(scale)
+        oh.copy_(od, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        return float(oh_np[0]), oh_np[1:].copy()
+    return evaluate
+
+
+def nnls_lbfgsb(inv, B):
+    """librosa.util.nnls(A, B) for a [M, T] float32 device block, the algorithm lib/wam_1D.py:446
+    runs: x_init = clip(pinv(A) @ B, 0) (float32, on the device); if the T columns fit
+    MAX_MEM_BLOCK one L-BFGS-B run over all of them, else one per block of lbfgsb_columns(M)
+    columns, each from its own columns of x_init; the float64 result rounded to float32.
+    -> [F, T] float32 on B's device."""
+    M, T = B.shape
+    x_init = torch.clamp(inv.pinv @ B, min=0.0)
+    n_col = lbfgsb_columns(M)
+    m = int(inv.A.shape[1])
+    if T <= n_col:
+        x = nnls_lbfgsb_block(device_objective(inv, B), x_init.cpu().numpy(), m)
+        return torch.from_numpy(x.astype(np.float32)).to(B.device)
+    x = x_init.clone()
+    for s0 in range(0, T, n_col):
+        s1 = min(s0 + n_col, T)
+        blk = nnls_lbfgsb_block(device_objective(inv, B[:, s0:s1].contiguous()), x_init[:, s0:s1].cpu().numpy(), m)
+        x[:, s0:s1] = torch.from_numpy(blk).to(B.device)
+    return x
+
+
 def nnls_mel(inv, B, max_iter=3000, tol=1e-6):
     """min_x 0.5 ||A x - B||^2 s.t. x >= 0, column by column, B [..., M, T] (device) -> x [..., F, T].
+    The exact minimiser (``nnls="exact"``; the default follows librosa: nnls_lbfgsb).
 
     librosa's nnls (the algorithm lib/wam_1D.py:446 runs) starts from the clipped minimum-norm
     least-squares solution and runs scipy's L-BFGS-B. Here every column of the batch runs FISTA
@@ -246,10 +327,20 @@ def nnls_mel(inv, B, max_iter=3000, tol=1e-6):
     return x.reshape(F, -1, T).permute(1, 0, 2).reshape(shape[:-2] + (F, T))
 
 
-def mel_to_stft(M, sample_rate, n_fft, power=2.0):
+NNLS_METHODS = ("lbfgsb", "exact")
+
+
+def mel_to_stft(M, sample_rate, n_fft, power=2.0, nnls="lbfgsb"):
     """librosa.feature.inverse.mel_to_stft(M, sr, n_fft) (power 2): NNLS of the Slaney mel basis,
-    then x ** (1 / power). M [..., n_mels, T] on the device."""
+    then x ** (1 / power) in float32. M [n_mels, T] (or [..., n_mels, T] with nnls="exact") on the
+    device. nnls="lbfgsb" (default) is librosa's solver (nnls_lbfgsb: the reference's result);
+    nnls="exact" returns the exact minimiser of the same problem (nnls_mel, batched FISTA)."""
     require_cuda(M, "mel spectrogram")
+    if nnls not in NNLS_METHODS:
+        raise ValueError("nnls must be one of %s, got %r" % (NNLS_METHODS, nnls))
     inv = MelInverse.get(sample_rate, n_fft, M.shape[-2], M.device)
-    x = nnls_mel(inv, M)
-    return x.pow(1.0 / power)
+    if nnls == "exact":
+        return nnls_mel(inv, M).pow(1.0 / power)
+    if M.dim() != 2:
+        raise ValueError("librosa's nnls takes one [n_mels, T] spectrogram per call, got %s" % (tuple(M.shape),))
+    return nnls_lbfgsb(inv, M.to(torch.float32).contiguous()).pow(1.0 / power)

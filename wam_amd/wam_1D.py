@@ -23,20 +23,29 @@ def normalize(data):
     return (data - np.min(data)) / (np.max(data) - np.min(data))
 
 
-def process_in_chunks(melspec, chunk_size, sr, n_fft):
+def process_in_chunks(melspec, chunk_size, sr, n_fft, nnls="lbfgsb"):
     """lib/wam_1D.py:442-448: librosa.feature.inverse.mel_to_stft of a [n_mels, T] power mel
-    spectrogram in time chunks of chunk_size frames -> [1 + n_fft // 2, T] magnitudes. The device
-    NNLS (wam_amd.melspec.mel_to_stft) solves every frame independently, so the chunks are one
-    batch here; chunk_size only keeps the reference's signature. Returns the exact NNLS minimiser:
-    it matches librosa's L-BFGS-B result in the re-projected mel spectrogram, not necessarily in the
-    magnitudes (see VisualizerWAM1D.compute_spectrogram)."""
+    spectrogram in time chunks of chunk_size frames, hstacked -> [1 + n_fft // 2, T] float32
+    magnitudes. Each chunk is one librosa NNLS problem (its objective is scaled by the chunk's own
+    size), solved as librosa solves it: clipped pinv start on the device, scipy's L-BFGS-B driving
+    float64 objective / gradient evaluations on the device (wam_amd.melspec.nnls_lbfgsb).
+    nnls="exact" (build-only keyword) returns the exact NNLS minimiser of every frame instead
+    (batched FISTA; the chunks are then one batch and chunk_size is only validated)."""
     from .melspec import mel_to_stft
-    if int(chunk_size) < 1:
+    chunk_size = int(chunk_size)
+    if chunk_size == 0:
         raise ValueError("range() arg 3 must not be zero")
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
     m = torch.as_tensor(np.asarray(melspec, dtype=np.float32))
     m = m.to(require_gpu_device(dev or "cpu"))
-    return mel_to_stft(m, sr, n_fft).cpu().numpy()
+    if nnls == "exact":
+        if chunk_size < 0:
+            raise ValueError("need at least one array to concatenate")
+        return mel_to_stft(m, sr, n_fft, nnls="exact").cpu().numpy()
+    parts = [mel_to_stft(m[:, i:i + chunk_size], sr, n_fft, nnls=nnls) for i in range(0, m.shape[1], chunk_size)]
+    if not parts:  # np.hstack([]) in the reference
+        raise ValueError("need at least one array to concatenate")
+    return torch.cat(parts, dim=1).cpu().numpy()
 
 
 def _peak_normalise(x):
@@ -304,9 +313,9 @@ class VisualizerWAM1D(WaveletAttribution1D):
     spectrogram. The reference's spectrograms come from librosa (absent offline, parity
     unpinned): ``spectrogram_from_waveform`` restates librosa.stft's magnitude (hann window,
     centred, constant padding -- librosa >= 0.10 -- hop n_fft // 4) with torch.stft on the GPU;
-    ``compute_spectrogram`` is librosa's mel_to_stft (NNLS of the Slaney mel basis, then sqrt) as a
-    batched device solver (wam_amd.melspec.nnls_mel), which ``filtered_spectrogram_from_melspec``
-    uses on the source and the filtered mel spectrograms."""
+    ``compute_spectrogram`` is librosa's mel_to_stft (NNLS of the Slaney mel basis by librosa's own
+    L-BFGS-B scheme, objective evaluated on the device, then sqrt; wam_amd.melspec.nnls_lbfgsb), which
+    ``filtered_spectrogram_from_melspec`` uses on the source and the filtered mel spectrograms."""
 
     def __init__(self, model, x, wavelet="haar", J=3, method="smooth", mode="reflect", device=None,
                  approx_coeffs=False, n_mels=128, n_fft=1024, sample_rate=44100, n_samples=25, stdev_spread=0.001,
@@ -326,22 +335,22 @@ class VisualizerWAM1D(WaveletAttribution1D):
         from .melspec import melspec_power
         return melspec_power(self._wave(x), self.n_fft, self.sample_rate, self.n_mels).cpu().numpy()
 
-    def compute_spectrogram(self, melspecs, chunk_size=100):
+    def compute_spectrogram(self, melspecs, chunk_size=100, nnls="lbfgsb"):
         """lib/wam_1D.py:478-488: the STFT magnitudes of power mel spectrograms [N, n_mels, T] by
-        librosa.feature.inverse.mel_to_stft (NNLS on librosa's Slaney mel basis, then sqrt), all
-        waveforms and frames in one device batch -> [N, 1 + n_fft // 2, T] float32.
-
-        The result is the exact NNLS minimiser (FISTA run to a KKT tolerance), not librosa's
-        L-BFGS-B iterate, which stops early at an absolute projected-gradient tolerance. The mel
-        basis has more bins than bands, so the minimiser is not unique: only the re-projected mel
-        spectrogram A x (and the objective) match librosa's; the magnitudes themselves can differ
-        in the basis' null space (tests/test_gpu_visual1d.py reports the gap). chunk_size is
-        validated and otherwise unused: every frame is solved on its own."""
+        librosa.feature.inverse.mel_to_stft per waveform, in chunks of chunk_size frames
+        (process_in_chunks) -> [N, 1 + n_fft // 2, T] float32: librosa's NNLS (clipped pinv start,
+        scipy L-BFGS-B over float64 objective evaluations on the device), i.e. the reference's
+        result. nnls="exact" (build-only keyword) returns the exact NNLS minimiser of every frame
+        (one batched device solve; not the reference's early-stopped iterate: the minimiser is not
+        unique and the two differ in the basis' null space)."""
         from .melspec import mel_to_stft
-        if int(chunk_size) < 1:
-            raise ValueError("range() arg 3 must not be zero")
-        m = torch.as_tensor(np.asarray(melspecs, dtype=np.float32)).to(self._dev)
-        return mel_to_stft(m, self.sample_rate, self.n_fft).cpu().numpy()
+        if nnls == "exact":
+            if int(chunk_size) < 1:
+                raise ValueError("range() arg 3 must not be zero")
+            m = torch.as_tensor(np.asarray(melspecs, dtype=np.float32)).to(self._dev)
+            return mel_to_stft(m, self.sample_rate, self.n_fft, nnls="exact").cpu().numpy()
+        return np.array([process_in_chunks(m, chunk_size, self.sample_rate, self.n_fft, nnls=nnls)
+                         for m in np.asarray(melspecs, dtype=np.float32)])
 
     def filter_melspec(self, audio_melspecs, grad_melspecs, filtering_method, EPS=0.2):
         """lib/wam_1D.py:491-519 (hard threshold of the min-max-normalised gradient, or modulation)."""
@@ -402,8 +411,10 @@ class VisualizerWAM1D(WaveletAttribution1D):
         sounds = self.filter_from_wavelet_coefficients(coeffs, grad_coeffs, filtering_method=filtering_method, EPS=EPS)
         return self.source_spectrograms, self.spectrogram_from_waveform(sounds)
 
-    def filtered_spectrogram_from_melspec(self, grad_melspecs, filtering_method, EPS=0.2, chunk_size=100):
+    def filtered_spectrogram_from_melspec(self, grad_melspecs, filtering_method, EPS=0.2, chunk_size=100,
+                                          nnls="lbfgsb"):
+        """lib/wam_1D.py:619-643 (nnls: build-only keyword, see compute_spectrogram)."""
         audio = self.compute_melspec(self.x)
-        self.source_spectrograms = self.compute_spectrogram(audio, chunk_size=chunk_size)
+        self.source_spectrograms = self.compute_spectrogram(audio, chunk_size=chunk_size, nnls=nnls)
         return self.source_spectrograms, self.compute_spectrogram(
-            self.filter_melspec(audio, grad_melspecs, filtering_method, EPS=EPS), chunk_size=chunk_size)
+            self.filter_melspec(audio, grad_melspecs, filtering_method, EPS=EPS), chunk_size=chunk_size, nnls=nnls)
