@@ -53,16 +53,19 @@ import tempfile
 import time
 
 # MIOpen picks the bf16 model's convolution solvers by timing them on a process's first use (about
-# a minute on a fresh box, and a noisy choice: some runs land 5 % slower). The bench
-# starts from the find database of an MI355X run instead (wam_amd/data/miopen: MIOpen's own
-# records, copied to a scratch directory it may update); a caller's MIOPEN_USER_DB_PATH wins.
+# a minute of warm-up on a fresh box). The bench starts from the find database of an
+# MI355X run instead (wam_amd/data/miopen: MIOpen's own records, copied to a scratch directory it may
+# update, removed at exit); this saves the solver timing, it does not remove the model's run-to-run
+# spread (605-628 attr/s at c2 with or without it). A caller's MIOPEN_USER_DB_PATH wins.
 if "MIOPEN_USER_DB_PATH" not in os.environ:
     _fdb = os.path.join(os.path.dirname(os.path.abspath(__file__)), "wam_amd", "data", "miopen")
     if os.path.isdir(_fdb):
+        import atexit
         _udb = tempfile.mkdtemp(prefix="wam_miopen_")
         for _f in os.listdir(_fdb):
             shutil.copy(os.path.join(_fdb, _f), _udb)
         os.environ["MIOPEN_USER_DB_PATH"] = _udb
+        atexit.register(shutil.rmtree, _udb, True)
 
 import numpy as np
 import torch
@@ -170,6 +173,8 @@ def parse(argv=None):
     ap.add_argument("--model-dtype", default=None, choices=["bf16", "fp32"], help="default: the config's")
     ap.add_argument("--sample-batch", type=int, default=None,
                     help="noise samples / IG steps per model call (default: ~832 images per call for c2/c4)")
+    ap.add_argument("--no-bf16-handoff", action="store_true",
+                    help="2D: fp32 model hand-off (cast / layout passes) instead of bf16 NHWC (A/B)")
     ap.add_argument("--no-optimize-model", action="store_true",
                     help="run the model as is under autocast instead of the BN-folded copy (model_opt.py)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
@@ -230,7 +235,8 @@ def build_explainer(wl, dev, args, model=None, dist_on=False, model_dtype=None, 
         sb = args.sample_batch or _auto_sample_batch(wl, n_local or wl.n)
         return wam_amd.WaveletAttribution2D(model, sample_batch=sb, autocast_dtype=ac, channels_last=cl,
                                             optimize_model=opt, dist=True if dist_on else None,
-                                            dist_axis=args.dist_axis or wl.dist_axis, **kw)
+                                            dist_axis=args.dist_axis or wl.dist_axis,
+                                            bf16_handoff=not args.no_bf16_handoff, **kw)
     if wl.dim == 1:
         return wam_amd.WaveletAttribution1D(model, sample_batch=args.sample_batch or 5, autocast_dtype=ac,
                                             dist=True if dist_on else None, **kw)

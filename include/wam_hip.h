@@ -108,7 +108,7 @@ int wam_waverec_adjoint(const wam_plan* plan, int64_t batch, const float* grad, 
 /* ------------------------------------------------------------------------------------------------
  * Fused WAM passes (2D, rows <= 512 samples, filter length in {2,4,6,8,12,16,20})
  * ---------------------------------------------------------------------------------------------- */
-enum wam_caps { WAM_CAP_NOISY_WAVEDEC = 1, WAM_CAP_ADJOINT_MAPS = 2 };
+enum wam_caps { WAM_CAP_NOISY_WAVEDEC = 1, WAM_CAP_ADJOINT_MAPS = 2, WAM_CAP_BF16_NHWC = 4 };
 /* which fused entry points below this plan supports (bit set of wam_caps) */
 int wam_plan_caps(const wam_plan* plan);
 
@@ -138,6 +138,23 @@ int wam_wavedec_noisy_ex(const wam_plan* plan, int64_t n_samples, int64_t images
 int wam_waverec_adjoint_maps(const wam_plan* plan, int64_t groups, int64_t group_items, int channels,
                              const float* grad, float* maps, float* band_max, float* coeff_grads,
                              void* workspace, void* stream);
+
+/* The model hand-off in the explained model's own dtype and layout (lib/wam_2D.py:113-116 with a
+ * bf16 channels-last model): wam_waverec_bf16_nhwc is wam_waverec whose reconstruction is written
+ * as bf16 images in NHWC order, out [n_alpha * batch / channels, H, W, channels] (plane b = image
+ * b / channels, channel b % channels), each value rounded to nearest even exactly as torch's
+ * float -> bfloat16 cast; wam_waverec_adjoint_maps_bf16_nhwc is wam_waverec_adjoint_maps over
+ * a bf16 NHWC input gradient grad [groups * group_items, H, W, channels] (values widened exactly;
+ * no coefficient gradients). Both need WAM_CAP_BF16_NHWC and channels in {1, 3}; no workspace. */
+int wam_waverec_bf16_nhwc(const wam_plan* plan, int64_t batch, const float* coeffs, const float* alpha,
+                          int n_alpha, int channels, void* out, void* stream);
+int wam_waverec_adjoint_maps_bf16_nhwc(const wam_plan* plan, int64_t groups, int64_t group_items, int channels,
+                                       const void* grad, float* maps, float* band_max, void* stream);
+/* the same for a bf16 gradient in either layout: nhwc != 0 as above, nhwc == 0 planar NCHW
+ * [groups * group_items, channels, H, W] (what a model whose first layer's backward ends in a
+ * planar op, e.g. a pixel shuffle, hands back) */
+int wam_waverec_adjoint_maps_bf16(const wam_plan* plan, int64_t groups, int64_t group_items, int channels, int nhwc,
+                                  const void* grad, float* maps, float* band_max, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Live per-launch timing (profiling aid used by bench.py). While enabled every kernel launch is

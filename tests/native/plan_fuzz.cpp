@@ -56,11 +56,15 @@ static void probe(int ndim, const int64_t* shape, int levels, int L, int mode, i
   for (int a = 0; a < ndim; ++a) CHECK(dims[a] >= shape[a] && dims[a] <= shape[a] + 1);
   for (int64_t batch : {int64_t(0), int64_t(1), int64_t(7), int64_t(4800)}) CHECK(wam_plan_workspace_bytes(p, batch) >= 0);
   const int caps = wam_plan_caps(p);  // the fused kernels' support predicates
-  CHECK((caps & ~(WAM_CAP_NOISY_WAVEDEC | WAM_CAP_ADJOINT_MAPS)) == 0);
+  CHECK((caps & ~(WAM_CAP_NOISY_WAVEDEC | WAM_CAP_ADJOINT_MAPS | WAM_CAP_BF16_NHWC)) == 0);
+  // the bf16 hand-off needs the fused maps pass
+  CHECK(!(caps & WAM_CAP_BF16_NHWC) || (caps & WAM_CAP_ADJOINT_MAPS));
   with_caps += caps != 0;
   // compute entry points refuse a host-only plan before touching any buffer
   float dummy[4] = {0, 0, 0, 0};
   CHECK(wam_wavedec(p, 1, dummy, dummy, dummy, nullptr) == WAM_ERR_INVALID_ARG);
+  CHECK(wam_waverec_bf16_nhwc(p, 3, dummy, nullptr, 1, 3, dummy, nullptr) == WAM_ERR_INVALID_ARG);
+  CHECK(wam_waverec_adjoint_maps_bf16_nhwc(p, 1, 1, 3, dummy, dummy, dummy, nullptr) == WAM_ERR_INVALID_ARG);
   CHECK(wam_waverec(p, 1, dummy, nullptr, 1, dummy, dummy, nullptr) == WAM_ERR_INVALID_ARG);
   CHECK(wam_waverec_adjoint(p, 1, dummy, dummy, dummy, nullptr) == WAM_ERR_INVALID_ARG);
   wam_plan_destroy(p);

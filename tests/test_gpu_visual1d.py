@@ -86,10 +86,13 @@ def _nnls_obj(A, x, B):
 
 
 # magnitudes vs the oracle's librosa restatement: the device evaluates the same float64 objective
-# in another summation order and starts from an fp32 GEMM pinv(A) @ B (ulp-level differences that
-# L-BFGS-B carries into its iterate), so the bar is a tolerance, not bit identity
-SPEC_REL_L2 = 1e-4
-SPEC_MAX_OVER_MAX = 1e-3
+# in another summation order and starts from its own fp32 GEMM pinv(A) @ B. L-BFGS-B carries a
+# one-ulp change of that start into up to ~7e-4 rel-L2 / 1e-2 of max of its result (one iteration
+# more or less before the projected-gradient stop; measured on the reference algorithm itself,
+# tests/test_oracle.py::test_librosa_lbfgsb_start_sensitivity), i.e. librosa's own result moves by
+# that much with the BLAS it runs on; typical cases agree to 1e-7
+SPEC_REL_L2 = 2e-3
+SPEC_MAX_OVER_MAX = 2e-2
 
 
 @pytest.mark.parametrize("sr,n_fft,n_mels,T", [(16000, 256, 32, 24), (16000, 1024, 128, 40), (44100, 512, 64, 17)])

@@ -219,9 +219,29 @@ def test_wam_budget_override():
     assert engine.wam_budget_bytes() >= 1 << 30
 
 
+def test_wam_budget_ranks_sharing_a_device(monkeypatch):
+    """two ranks on one device (LOCAL_WORLD_SIZE 2, one visible device) each claim half of
+    the half of the free memory they both see; one rank per device claims the half."""
+    class Props:
+        total_memory = 288 << 30
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda d=None: Props())
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda d=None: (100 << 30, 288 << 30))
+    monkeypatch.setattr(torch.cuda, "memory_reserved", lambda d=None: 0)
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda d=None: 0)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert engine.ranks_per_device() == 1 and engine.wam_budget_bytes() == 36 << 30
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    assert engine.ranks_per_device() == 2 and engine.wam_budget_bytes() == 24 << 30
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert engine.ranks_per_device() == 1 and engine.wam_budget_bytes() == 36 << 30
+
+
 def test_wam_budget_tiers(monkeypatch):
     """The default budget is rounded to a tier, so a call's split into passes does not drift with
-    the allocator; ranks sharing a device are not divided twice (free memory already counts them)."""
+    the allocator."""
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
     assert engine.budget_tier(36 << 30) == 36 << 30
     assert engine.budget_tier((37 << 30) + 12345) == 36 << 30

@@ -69,6 +69,9 @@ _SIGS = {
     "wam_wavedec_noisy_ex": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, ctypes.c_uint64, c_i64, c_i64, c_vp, c_vp,
                                      c_vp]),
     "wam_waverec_adjoint_maps": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "wam_waverec_bf16_nhwc": (c_int, [c_vp, c_i64, c_vp, ctypes.POINTER(c_f32), c_int, c_int, c_vp, c_vp]),
+    "wam_waverec_adjoint_maps_bf16_nhwc": (c_int, [c_vp, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "wam_waverec_adjoint_maps_bf16": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "wam_timing_enable": (c_int, [c_int]),
     "wam_copy": (c_int, [c_i64, c_vp, c_vp, c_vp]),
     "wam_visualize3d": (c_int, [c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),

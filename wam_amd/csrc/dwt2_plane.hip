@@ -106,10 +106,71 @@ __device__ __forceinline__ float wave_max(float m) {
   return m;
 }
 
+// Input formats of the COOP maps pass: fp32 planes, or the explained model's own bf16 input gradient
+// in NHWC (channels_last) or NCHW order (widened on use: exact)
+enum { kInF32 = 0, kInBf16Nhwc = 1, kInBf16Nchw = 2 };
+
+// One source row of the COOP level 1 in registers (lane l: columns 4l .. 4l+3 of every channel).
+// fp32: NCH planar rows, 16-byte loads. bf16 NHWC: the image row, channels interleaved, NCH * 8 bytes
+// per lane; bf16 NCHW: NCH planar rows, 8 bytes per lane each.
+// Loads stay in flight until v() is first used (clamped addresses, validity applied on use).
+template <int NCH, int FMT>
+struct CoopRow {
+  RowRegs<4, 1> r[NCH];
+  __device__ __forceinline__ void fetch(const float* src, int64_t in_plane, int row, int nw, int lane, bool valid) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) r[c].fetch(src + c * in_plane + (int64_t)row * nw, nw, lane, valid);
+  }
+  __device__ __forceinline__ bool ok() const { return r[0].ok[0]; }
+  __device__ __forceinline__ float v(int c, int k) const { return r[c].v[k]; }
+};
+
+template <int NCH>
+struct CoopRow<NCH, kInBf16Nhwc> {
+  uint2 raw[NCH];  // 4 * NCH bf16 values: pixel k, channel c at element k * NCH + c
+  bool okv;
+  __device__ __forceinline__ void fetch(const float* src, int64_t, int row, int nw, int lane, bool valid) {
+    const int idx = lane * 4;
+    okv = valid && idx < nw;
+    const int ci = idx < nw ? idx : nw - 4;
+    const uint2* p = reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(src) +
+                                                    ((int64_t)row * nw + ci) * NCH);
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) raw[k] = p[k];
+  }
+  __device__ __forceinline__ bool ok() const { return okv; }
+  __device__ __forceinline__ float v(int c, int k) const {
+    const int e = k * NCH + c;  // static after unrolling
+    const uint32_t w = (e & 2) ? raw[e >> 2].y : raw[e >> 2].x;
+    return __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
+  }
+};
+
+template <int NCH>
+struct CoopRow<NCH, kInBf16Nchw> {
+  uint2 raw[NCH];  // channel c: pixels 4l .. 4l+3 of its plane's row
+  bool okv;
+  __device__ __forceinline__ void fetch(const float* src, int64_t in_plane, int row, int nw, int lane, bool valid) {
+    const int idx = lane * 4;
+    okv = valid && idx < nw;
+    const int ci = idx < nw ? idx : nw - 4;
+    const uint16_t* b = reinterpret_cast<const uint16_t*>(src) + (int64_t)row * nw + ci;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) raw[c] = *reinterpret_cast<const uint2*>(b + c * in_plane);
+  }
+  __device__ __forceinline__ bool ok() const { return okv; }
+  __device__ __forceinline__ float v(int c, int k) const {
+    const uint32_t w = (k & 2) ? raw[c].y : raw[c].x;
+    return __uint_as_float((k & 1) ? (w & 0xffff0000u) : (w << 16));
+  }
+};
+
 // MC: 0 = one input plane per item; C > 0 = item is an image of C planes, averaged on load
 // CPL: level-1 output columns per lane (mw <= 64 * CPL): one wave covers a whole row
 // COOP: level 1 as a cooperative row stream (see phase 1 below) instead of wave-private chunks
-template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP>
+// IN (COOP maps only for the bf16 formats): kInF32, or bf16 images [items, nh, nw, MC] (kInBf16Nhwc)
+// / [items, MC, nh, nw] (kInBf16Nchw)
+template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP, int IN = kInF32>
 __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))) k_plane_ana(const float* __restrict__ in, float* __restrict__ out,
                                                    float* __restrict__ band_max, const float* __restrict__ filt,
                                                    PlaneGeom g, WamNoise nz, int64_t n_items, int64_t S,
@@ -149,7 +210,10 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     ch = src_plane % nz.channels;
     sg = nz.sigma[img];
   }
-  const float* src = in + src_plane * (int64_t)NCH * in_plane;
+  static_assert(IN == kInF32 || (COOP && MAPS && !NOISE), "bf16 input: COOP maps pass only");
+  const float* src = IN != kInF32 ? reinterpret_cast<const float*>(reinterpret_cast<const uint16_t*>(in) +
+                                                                   src_plane * (int64_t)NCH * in_plane)
+                                  : in + src_plane * (int64_t)NCH * in_plane;
 
   typedef float f2 __attribute__((ext_vector_type(2)));
   f2 fh2[L];  // (lo, hi) tap pairs for packed fp32 FMAs
@@ -214,31 +278,30 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     const int nb = (mh + RB - 1) / RB;
     float mx[4] = {0.f, 0.f, 0.f, 0.f};
 
-    auto fetch = [&](RowRegs<4, 1> (&fr)[NCH], int& sr_out, int e) {
+    using CRow = CoopRow<NCH, IN>;
+    auto fetch = [&](CRow& fr, int& sr_out, int e) {
       const int sr = row_src(e, nh, mode);
       const bool valid = sr >= 0;
       sr_out = sr;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) fr[c].fetch(src + c * in_plane + (int64_t)(valid ? sr : 0) * nw, nw, lane, valid);
+      fr.fetch(src, in_plane, valid ? sr : 0, nw, lane, valid);
     };
     // horizontal pass of ext row e into its ring slot (nzr: its noise, from noise2)
-    auto hrow = [&](RowRegs<4, 1> (&fr)[NCH], int sr, int e, const float (&nzr)[4]) {
-      float4 o = fr[0].ok[0] ? make_float4(fr[0].v[0], fr[0].v[1], fr[0].v[2], fr[0].v[3])
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    auto hrow = [&](CRow& fr, int sr, int e, const float (&nzr)[4]) {
+      float4 o = fr.ok() ? make_float4(fr.v(0, 0), fr.v(0, 1), fr.v(0, 2), fr.v(0, 3)) : make_float4(0.f, 0.f, 0.f, 0.f);
       if constexpr (NCH > 1) {
 #pragma unroll
         for (int c = 1; c < NCH; ++c) {
-          o.x += fr[c].v[0];
-          o.y += fr[c].v[1];
-          o.z += fr[c].v[2];
-          o.w += fr[c].v[3];
+          o.x += fr.v(c, 0);
+          o.y += fr.v(c, 1);
+          o.z += fr.v(c, 2);
+          o.w += fr.v(c, 3);
         }
         constexpr float inv = 1.0f / (float)NCH;
         o.x *= inv;
         o.y *= inv;
         o.z *= inv;
         o.w *= inv;
-        if (!fr[0].ok[0]) o = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!fr.ok()) o = make_float4(0.f, 0.f, 0.f, 0.f);
       }
       if constexpr (NOISE) {
         // zero rows (sr < 0, wave-uniform) stay zero: fma(0, z, 0) with a finite z
@@ -318,10 +381,10 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     };
 
     // prologue: ext rows -p .. -1 (waves 0 .. p-1, one each) and the first D blocks in flight
-    RowRegs<4, 1> fp[NCH];
+    CRow fp;
     int spro;
     fetch(fp, spro, wv < p ? wv - p : -p);
-    RowRegs<4, 1> F[D][2][NCH];
+    CRow F[D][2];
     int S[D][2];
 #pragma unroll
     for (int u = 0; u < D; ++u) {
@@ -819,10 +882,14 @@ __device__ __forceinline__ bool syn_work(int oh, int ow, int wv, int& strip, int
   return chunk < chunks && qbeg < qend;
 }
 
-template <int L>
+// OC: output format of level 0: 0 = fp32 planes [items, oh, ow]; C = 1 or 3: bf16 images in NHWC
+// order [items / C, oh, ow, C] (item = image * C + channel; the explained model's own input dtype and
+// layout, rounded as torch's fp32 -> bf16 cast rounds)
+template <int L, int OC = 0>
 __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8)))
-    k_plane_syn(const float* __restrict__ coeffs, float* __restrict__ out, const float* __restrict__ filt, SynGeom g,
+    k_plane_syn(const float* __restrict__ coeffs, void* __restrict__ out_v, const float* __restrict__ filt, SynGeom g,
                 SynAlphas al, int64_t n_items) {
+  float* out = static_cast<float*>(out_v);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int64_t nwg = gridDim.x, bid = blockIdx.x;
   const int64_t q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
@@ -853,12 +920,22 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     if (!syn_work<L>(oh, ow, wv, strip, qbeg, qend)) continue;
     const bool coarsest = l == g.J - 1;
     if (l == 0) {
-      float* dst = out + (g.out_base + (int64_t)ai * g.batch + item) * ((int64_t)oh * ow);
-      if (coarsest)
-        syn_stream<L>(coeffs + g.batch * g.off_a + item * bn, s, pH, pV, pD, s, mh, mw, dst, oh, ow, strip, qbeg,
-                      qend, xch, rlo, rhi, lane);
-      else
-        syn_stream<L>(bufL, 1.f, pH, pV, pD, s, mh, mw, dst, oh, ow, strip, qbeg, qend, xch, rlo, rhi, lane);
+      const int64_t oi = g.out_base + (int64_t)ai * g.batch + item;
+      if constexpr (OC == 0) {
+        float* dst = out + oi * ((int64_t)oh * ow);
+        if (coarsest)
+          syn_stream<L>(coeffs + g.batch * g.off_a + item * bn, s, pH, pV, pD, s, mh, mw, dst, oh, ow, strip, qbeg,
+                        qend, xch, rlo, rhi, lane);
+        else
+          syn_stream<L>(bufL, 1.f, pH, pV, pD, s, mh, mw, dst, oh, ow, strip, qbeg, qend, xch, rlo, rhi, lane);
+      } else {
+        const SynOutBf16<OC> dst{static_cast<uint16_t*>(out_v) + (oi / OC) * ((int64_t)oh * ow * OC) + oi % OC};
+        if (coarsest)
+          syn_stream_to<L>(coeffs + g.batch * g.off_a + item * bn, s, pH, pV, pD, s, mh, mw, dst, oh, ow, strip,
+                           qbeg, qend, xch, rlo, rhi, lane);
+        else
+          syn_stream_to<L>(bufL, 1.f, pH, pV, pD, s, mh, mw, dst, oh, ow, strip, qbeg, qend, xch, rlo, rhi, lane);
+      }
     } else {
       float* dst = (l & 1) ? bufL : bufS;
       if (coarsest)
@@ -969,11 +1046,11 @@ PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items
   return g;
 }
 
-template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP>
+template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP, int IN = kInF32>
 int launch_plane_t(const PlaneGeom& g, int lds_bytes, int64_t n_items, const float* in, float* out, float* band_max,
                    const float* filt, const WamNoise& nz, int64_t S, int64_t group_items, const char* name,
                    double bytes, hipStream_t st) {
-  auto kern = k_plane_ana<L, CPL, NOISE, MC, MAPS, COOP>;
+  auto kern = k_plane_ana<L, CPL, NOISE, MC, MAPS, COOP, IN>;
   static std::atomic<uint64_t> attr_set{0};  // opt in to > 64 KB of dynamic LDS, once per device
   int dev = 0;
   WAM_HIP_CHECK(hipGetDevice(&dev));
@@ -1011,7 +1088,33 @@ int dispatch_plane(const wam_plan* p, const PlaneGeom& g, int lds_bytes, int64_t
 #undef WAM_PLANE_ARGS
 }
 
+// the maps pass over bf16 input gradients (COOP level 1 only)
+template <int MC, int IN>
+int dispatch_maps_bf16(const wam_plan* p, const PlaneGeom& g, int lds_bytes, int64_t n_items, const float* in,
+                       float* out, float* band_max, const float* filt, int64_t group_items, double bytes,
+                       hipStream_t st) {
+  if (!g.coop) return WAM_ERR_UNSUPPORTED;
+  const WamNoise nz{nullptr, 1, 1, 0, 0, 0, 0};
+  const bool two = g.mw[0] > 64;
+  const char* name = IN == kInBf16Nhwc ? "k_plane_maps<bf16nhwc>" : "k_plane_maps<bf16>";
+#define WAM_MAPS_CASE(LL)                                                                                          \
+  case LL:                                                                                                         \
+    return two ? launch_plane_t<LL, 2, false, MC, true, true, IN>(g, lds_bytes, n_items, in, out, band_max, filt,  \
+                                                                   nz, 1, group_items, name, bytes, st)             \
+               : launch_plane_t<LL, 1, false, MC, true, true, IN>(g, lds_bytes, n_items, in, out, band_max, filt,  \
+                                                                   nz, 1, group_items, name, bytes, st);
+  switch (p->L) {
+    WAM_MAPS_CASE(2) WAM_MAPS_CASE(4) WAM_MAPS_CASE(6) WAM_MAPS_CASE(8)
+    default: return WAM_ERR_UNSUPPORTED;
+  }
+#undef WAM_MAPS_CASE
+}
+
 }  // namespace
+
+bool dwt2_plane_maps_coop(const wam_plan* p) {
+  return dwt2_plane_supported(p, true) && coop_ok(p, (int)p->rec_shape[1]);
+}
 
 bool dwt2_plane_supported(const wam_plan* p, bool adjoint) {
   const int nh0 = (int)(adjoint ? p->rec_shape[0] : p->lin[0][0]);
@@ -1043,8 +1146,9 @@ int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in
                                          "k_plane_ana", bytes, st);
 }
 
-int launch_dwt2_plane_maps(const wam_plan* p, int64_t images, int channels, int64_t group_items, const float* grad,
-                           float* maps, float* band_max, hipStream_t st) {
+int launch_dwt2_plane_maps(const wam_plan* p, int64_t images, int channels, int64_t group_items, const void* grad_v,
+                           int in_fmt, float* maps, float* band_max, hipStream_t st) {
+  const float* grad = static_cast<const float*>(grad_v);
   if (((uintptr_t)grad & 15) || !dwt2_plane_supported(p, true)) return WAM_ERR_UNSUPPORTED;
   if (channels != 1 && channels != 3) return WAM_ERR_UNSUPPORTED;
   const int nh0 = (int)p->rec_shape[0], nw0 = (int)p->rec_shape[1];
@@ -1053,7 +1157,14 @@ int launch_dwt2_plane_maps(const wam_plan* p, int64_t images, int channels, int6
   int rowlds, llcap;
   const int lds_bytes = lds_floats(p, nw0, rowlds, llcap) * 4;
   const WamNoise none{nullptr, 1, 1, 0, 0, 0, 0};
-  const double bytes = 4.0 * (double)images * ((double)channels * nh0 * nw0 + (double)p->band_off[p->nbands]);
+  const double bytes = (double)images * ((in_fmt ? 2.0 : 4.0) * channels * nh0 * nw0 +
+                                          4.0 * (double)p->band_off[p->nbands]);
+  if (in_fmt == kInBf16Nhwc && channels == 3)
+    return dispatch_maps_bf16<3, kInBf16Nhwc>(p, g, lds_bytes, images, grad, maps, band_max, filt, group_items, bytes, st);
+  if (in_fmt == kInBf16Nchw && channels == 3)
+    return dispatch_maps_bf16<3, kInBf16Nchw>(p, g, lds_bytes, images, grad, maps, band_max, filt, group_items, bytes, st);
+  if (in_fmt != kInF32)  // one channel: the two bf16 layouts coincide
+    return dispatch_maps_bf16<1, kInBf16Nchw>(p, g, lds_bytes, images, grad, maps, band_max, filt, group_items, bytes, st);
   if (channels == 3)
     return dispatch_plane<false, 3, true>(p, g, lds_bytes, images, grad, maps, band_max, filt, none, 1, group_items,
                                           "k_plane_maps", bytes, st);
@@ -1082,10 +1193,10 @@ bool syn_ok(const wam_plan* p) {
   return (int64_t)syn_lds_floats(p, lcap, scap) * 4 <= kPlaneLdsCap;
 }
 
-template <int L>
-int launch_syn_plane_t(const SynGeom& g, int lds_bytes, int64_t n_items, const float* coeffs, float* out,
+template <int L, int OC>
+int launch_syn_plane_t(const SynGeom& g, int lds_bytes, int64_t n_items, const float* coeffs, void* out,
                        const float* filt, const SynAlphas& al, double bytes, hipStream_t st) {
-  auto kern = k_plane_syn<L>;
+  auto kern = k_plane_syn<L, OC>;
   static std::atomic<uint64_t> attr_set{0};
   int dev = 0;
   WAM_HIP_CHECK(hipGetDevice(&dev));
@@ -1101,13 +1212,27 @@ int launch_syn_plane_t(const SynGeom& g, int lds_bytes, int64_t n_items, const f
   return WAM_OK;
 }
 
+template <int OC>
+int syn_plane_l(int L, const SynGeom& g, int lds_bytes, int64_t n_items, const float* coeffs, void* out,
+                const float* filt, const SynAlphas& al, double bytes, hipStream_t st) {
+  switch (L) {
+    case 2: return launch_syn_plane_t<2, OC>(g, lds_bytes, n_items, coeffs, out, filt, al, bytes, st);
+    case 4: return launch_syn_plane_t<4, OC>(g, lds_bytes, n_items, coeffs, out, filt, al, bytes, st);
+    case 6: return launch_syn_plane_t<6, OC>(g, lds_bytes, n_items, coeffs, out, filt, al, bytes, st);
+    case 8: return launch_syn_plane_t<8, OC>(g, lds_bytes, n_items, coeffs, out, filt, al, bytes, st);
+    default: return WAM_ERR_UNSUPPORTED;
+  }
+}
+
 }  // namespace
 
 bool dwt2_plane_syn_supported(const wam_plan* p) { return syn_ok(p); }
 
 int launch_dwt2_plane_synthesis(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha,
-                                int n_alpha, float* out, hipStream_t st) {
+                                int n_alpha, void* out, int out_channels, hipStream_t st) {
   if (!syn_ok(p)) return WAM_ERR_UNSUPPORTED;
+  if (out_channels != 0 && (out_channels != 1 && out_channels != 3)) return WAM_ERR_UNSUPPORTED;
+  if (out_channels && batch % out_channels) return WAM_ERR_INVALID_ARG;
   SynGeom g{};
   g.J = p->levels;
   for (int l = 0; l < p->levels; ++l) {
@@ -1128,16 +1253,13 @@ int launch_dwt2_plane_synthesis(const wam_plan* p, int64_t batch, const float* c
     for (int i = 0; i < na; ++i) al.v[i] = alpha ? alpha[a0 + i] : 1.0f;
     g.n_alpha = na;
     g.out_base = (int64_t)a0 * batch;
-    // algorithmic bytes: the coefficients once, every reconstruction once
-    const double bytes = 4.0 * ((double)batch * p->band_off[p->nbands] + (double)na * batch * out_item);
-    int rc;
-    switch (p->L) {
-      case 2: rc = launch_syn_plane_t<2>(g, lds_bytes, batch * na, coeffs, out, filt, al, bytes, st); break;
-      case 4: rc = launch_syn_plane_t<4>(g, lds_bytes, batch * na, coeffs, out, filt, al, bytes, st); break;
-      case 6: rc = launch_syn_plane_t<6>(g, lds_bytes, batch * na, coeffs, out, filt, al, bytes, st); break;
-      case 8: rc = launch_syn_plane_t<8>(g, lds_bytes, batch * na, coeffs, out, filt, al, bytes, st); break;
-      default: rc = WAM_ERR_UNSUPPORTED;
-    }
+    // algorithmic bytes: the coefficients once, every reconstruction once (2 B per bf16 pixel)
+    const double bytes = 4.0 * (double)batch * p->band_off[p->nbands] +
+                         (out_channels ? 2.0 : 4.0) * (double)na * batch * out_item;
+    const int64_t ni = batch * na;
+    const int rc = out_channels == 3   ? syn_plane_l<3>(p->L, g, lds_bytes, ni, coeffs, out, filt, al, bytes, st)
+                   : out_channels == 1 ? syn_plane_l<1>(p->L, g, lds_bytes, ni, coeffs, out, filt, al, bytes, st)
+                                       : syn_plane_l<0>(p->L, g, lds_bytes, ni, coeffs, out, filt, al, bytes, st);
     if (rc) return rc;
   }
   return WAM_OK;

@@ -63,13 +63,17 @@ struct WamNoise {
 
 // plane-resident multi-level 2D analysis (dwt2_plane.hip): all levels of a plane in one workgroup
 bool dwt2_plane_supported(const wam_plan* p, bool adjoint);
+bool dwt2_plane_maps_coop(const wam_plan* p);  // the maps pass runs the COOP level 1 (bf16 input possible)
 int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in, float* coeffs, bool adjoint,
                                const WamNoise* nz, int64_t n_samples, hipStream_t st);
-int launch_dwt2_plane_maps(const wam_plan* p, int64_t images, int channels, int64_t group_items, const float* grad,
-                           float* maps, float* band_max, hipStream_t st);
+// grad (in_fmt): 0 = fp32 planes [images, channels, nh, nw]; 1 = bf16 images [images, nh, nw, channels];
+// 2 = bf16 planes [images, channels, nh, nw]
+int launch_dwt2_plane_maps(const wam_plan* p, int64_t images, int channels, int64_t group_items, const void* grad,
+                           int in_fmt, float* maps, float* band_max, hipStream_t st);
 bool dwt2_plane_syn_supported(const wam_plan* p);
+// out_channels 0: fp32 planes; 1 or 3: bf16 NHWC images (planes = images x out_channels)
 int launch_dwt2_plane_synthesis(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha,
-                                int n_alpha, float* out, hipStream_t st);
+                                int n_alpha, void* out, int out_channels, hipStream_t st);
 
 // fused multi-level 1D tiles (dwt1_tile.hip)
 bool dwt1_tile_supported(const wam_plan* p, bool adjoint);

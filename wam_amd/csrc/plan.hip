@@ -469,6 +469,10 @@ int wam_plan_caps(const wam_plan* p) {
     caps |= WAM_CAP_NOISY_WAVEDEC;  // single-channel signals (channels != 1: WAM_ERR_UNSUPPORTED)
   if (p->ndim == 3 && !(p->flags & WAM_PLAN_GENERIC) && dwt3_haar_supported(p) && p->lin[0][2] % 4 == 0)
     caps |= WAM_CAP_NOISY_WAVEDEC;  // single-channel volumes (channels != 1: WAM_ERR_UNSUPPORTED)
+  // the bf16 NHWC model hand-off: plane-resident synthesis and the COOP maps pass of the plane kernel
+  if (p->ndim == 2 && !(p->flags & (WAM_PLAN_GENERIC | WAM_PLAN_NO_ROWS | WAM_PLAN_NO_PLANE)) &&
+      dwt2_plane_syn_supported(p) && use_plane(p, true) && dwt2_plane_maps_coop(p))
+    caps |= WAM_CAP_BF16_NHWC;
   return caps;
 }
 
@@ -500,7 +504,7 @@ int wam_waverec_adjoint_maps(const wam_plan* p, int64_t groups, int64_t group_it
   const int64_t planes = images * channels;
   if (use_plane(p, true)) {
     // maps from the channel-mean gradient (one pass); per-channel grads only when asked for
-    int rc = launch_dwt2_plane_maps(p, images, channels, group_items, grad, maps, band_max, st);
+    int rc = launch_dwt2_plane_maps(p, images, channels, group_items, grad, 0, maps, band_max, st);
     if (rc != WAM_ERR_UNSUPPORTED) {
       if (rc || !coeff_grads) return rc;
       return analysis_driver(p, planes, grad, coeff_grads, ws, st, true);
@@ -527,6 +531,32 @@ int wam_waverec_adjoint_maps(const wam_plan* p, int64_t groups, int64_t group_it
   return WAM_OK;
 }
 
+int wam_waverec_bf16_nhwc(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha, int n_alpha,
+                          int channels, void* out, void* stream) {
+  if (!p || !p->d_filt || !coeffs || !out || batch < 0 || n_alpha < 1 || channels < 1) return WAM_ERR_INVALID_ARG;
+  if (!alpha && n_alpha != 1) return WAM_ERR_INVALID_ARG;
+  if (!(wam_plan_caps(p) & WAM_CAP_BF16_NHWC) || (channels != 1 && channels != 3)) return WAM_ERR_UNSUPPORTED;
+  if (batch % channels) return WAM_ERR_INVALID_ARG;
+  if (batch == 0) return WAM_OK;
+  return launch_dwt2_plane_synthesis(p, batch, coeffs, alpha, n_alpha, out, channels, (hipStream_t)stream);
+}
+
+int wam_waverec_adjoint_maps_bf16(const wam_plan* p, int64_t groups, int64_t group_items, int channels, int nhwc,
+                                  const void* grad, float* maps, float* band_max, void* stream) {
+  if (!p || !p->d_filt || !grad || !maps || !band_max || groups < 0 || group_items < 0 || channels < 1)
+    return WAM_ERR_INVALID_ARG;
+  if (!(wam_plan_caps(p) & WAM_CAP_BF16_NHWC) || (channels != 1 && channels != 3)) return WAM_ERR_UNSUPPORTED;
+  const int64_t images = groups * group_items;
+  if (images == 0) return WAM_OK;
+  return launch_dwt2_plane_maps(p, images, channels, group_items, grad, nhwc ? 1 : 2, maps, band_max,
+                                (hipStream_t)stream);
+}
+
+int wam_waverec_adjoint_maps_bf16_nhwc(const wam_plan* p, int64_t groups, int64_t group_items, int channels,
+                                       const void* grad, float* maps, float* band_max, void* stream) {
+  return wam_waverec_adjoint_maps_bf16(p, groups, group_items, channels, 1, grad, maps, band_max, stream);
+}
+
 int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha, int n_alpha, float* out,
                 void* ws, void* stream) {
   if (!p || !p->d_filt || !coeffs || !out || !ws || batch < 0 || n_alpha < 1) return WAM_ERR_INVALID_ARG;
@@ -535,7 +565,7 @@ int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const flo
   hipStream_t st = (hipStream_t)stream;
   if (p->ndim == 2 && !(p->flags & (WAM_PLAN_GENERIC | WAM_PLAN_NO_ROWS | WAM_PLAN_NO_PLANE)) &&
       dwt2_plane_syn_supported(p)) {  // all levels and all alphas in one launch
-    int rc = launch_dwt2_plane_synthesis(p, batch, coeffs, alpha, n_alpha, out, st);
+    int rc = launch_dwt2_plane_synthesis(p, batch, coeffs, alpha, n_alpha, out, 0, st);
     if (rc != WAM_ERR_UNSUPPORTED) return rc;
   }
   if (p->ndim == 1 && !(p->flags & WAM_PLAN_GENERIC)) {

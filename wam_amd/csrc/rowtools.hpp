@@ -185,12 +185,43 @@ __device__ __forceinline__ void syn_fma2(F2& acc, F2 w, float x) {
 // register ring, lcm(H2, PF) rows per iteration (sym8 at 512^2: 444 -> 353 us per 2-alpha finest
 // level). Short filters keep scalar chains and a shifted ring: the memory-bound plane synthesis
 // measured 447 vs 439 us in the static-ring form (profiles/r03j_kbench_syn_ab.log)
-template <int L, int PF = kSynPF, bool PK = (L >= 12)>
-__device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float sa, const float* __restrict__ pH,
-                                           const float* __restrict__ pV, const float* __restrict__ pD, float sd,
-                                           int mh, int mw, float* __restrict__ dst, int oh, int ow, int strip,
-                                           int qbeg, int qend, float4* xch, const float (&rlo)[L],
-                                           const float (&rhi)[L], int lane, bool vec2 = true) {
+// Output sinks of syn_stream: where the reconstructed pixels of a level go (element index idx =
+// row * ow + column of the level's output plane).
+struct SynOutF32 {  // fp32 plane, row-major (HBM or LDS); a pixel pair as one 8-byte store
+  float* dst;
+  __device__ __forceinline__ void pair(unsigned idx, float a, float b) const {
+    *reinterpret_cast<float2*>(at32(dst, idx)) = make_float2(a, b);
+  }
+  __device__ __forceinline__ void one(unsigned idx, float a) const { *at32(dst, idx) = a; }
+};
+
+// fp32 -> bf16, round to nearest even, NaN -> 0x7FC0: torch's float -> BFloat16 conversion bit for bit
+__device__ __forceinline__ uint16_t bf16_rne(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return f != f ? (uint16_t)0x7FC0u : (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
+// bf16 channel-interleaved plane (NHWC with C channels): pixel idx of this channel at dst[idx * C]
+// (dst = image base + channel). The C channel planes of an image are reconstructed by C
+// neighbouring workgroups of one XCD, so their partial-line stores meet in that XCD's L2.
+template <int C>
+struct SynOutBf16 {
+  uint16_t* dst;
+  __device__ __forceinline__ void one(unsigned idx, float a) const {
+    *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(dst) + 2u * C * idx) = bf16_rne(a);
+  }
+  __device__ __forceinline__ void pair(unsigned idx, float a, float b) const {
+    one(idx, a);
+    one(idx + 1, b);
+  }
+};
+
+template <int L, int PF = kSynPF, bool PK = (L >= 12), class Out = SynOutF32>
+__device__ __forceinline__ void syn_stream_to(const float* __restrict__ pA, float sa, const float* __restrict__ pH,
+                                              const float* __restrict__ pV, const float* __restrict__ pD, float sd,
+                                              int mh, int mw, const Out dst, int oh, int ow, int strip,
+                                              int qbeg, int qend, float4* xch, const float (&rlo)[L],
+                                              const float (&rhi)[L], int lane, bool vec2 = true) {
   constexpr int p = L - 2;
   constexpr int H2 = L / 2;
   constexpr int OUTQ = 65 - H2;
@@ -279,25 +310,25 @@ __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float s
               // the common case in one block: both chains are used by it, so the compiler keeps
               // them interleaved (with a store branch per row it sank each 2 H2-deep dependent
               // chain into its own branch, back to back)
-              *reinterpret_cast<float2*>(at32(dst, (unsigned)(r0 * ow + ucol))) = make_float2(o0.x, o0.y);
-              *reinterpret_cast<float2*>(at32(dst, (unsigned)((r0 + 1) * ow + ucol))) = make_float2(o1.x, o1.y);
+              dst.pair((unsigned)(r0 * ow + ucol), o0.x, o0.y);
+              dst.pair((unsigned)((r0 + 1) * ow + ucol), o1.x, o1.y);
             } else {
               if (r0 < oh) {
-                float* d0 = at32(dst, (unsigned)(r0 * ow + ucol));
+                const unsigned d0 = (unsigned)(r0 * ow + ucol);
                 if (pair) {
-                  *reinterpret_cast<float2*>(d0) = make_float2(o0.x, o0.y);
+                  dst.pair(d0, o0.x, o0.y);
                 } else {
-                  d0[0] = o0.x;
-                  if (two) d0[1] = o0.y;
+                  dst.one(d0, o0.x);
+                  if (two) dst.one(d0 + 1, o0.y);
                 }
               }
               if (r0 + 1 < oh) {
-                float* d1 = at32(dst, (unsigned)((r0 + 1) * ow + ucol));
+                const unsigned d1 = (unsigned)((r0 + 1) * ow + ucol);
                 if (pair) {
-                  *reinterpret_cast<float2*>(d1) = make_float2(o1.x, o1.y);
+                  dst.pair(d1, o1.x, o1.y);
                 } else {
-                  d1[0] = o1.x;
-                  if (two) d1[1] = o1.y;
+                  dst.one(d1, o1.x);
+                  if (two) dst.one(d1 + 1, o1.y);
                 }
               }
             }
@@ -360,25 +391,25 @@ __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float s
           if (ucol >= 0 && ucol < ow) {
             const bool two = ucol + 1 < ow, pair = two && vec2;
             if (pair && r0 + 1 < oh) {  // the common case in one block (see the PK form)
-              *reinterpret_cast<float2*>(at32(dst, (unsigned)(r0 * ow + ucol))) = make_float2(o00, o01);
-              *reinterpret_cast<float2*>(at32(dst, (unsigned)((r0 + 1) * ow + ucol))) = make_float2(o10, o11);
+              dst.pair((unsigned)(r0 * ow + ucol), o00, o01);
+              dst.pair((unsigned)((r0 + 1) * ow + ucol), o10, o11);
             } else {
               if (r0 < oh) {
-                float* d0 = at32(dst, (unsigned)(r0 * ow + ucol));
+                const unsigned d0 = (unsigned)(r0 * ow + ucol);
                 if (pair) {
-                  *reinterpret_cast<float2*>(d0) = make_float2(o00, o01);
+                  dst.pair(d0, o00, o01);
                 } else {
-                  d0[0] = o00;
-                  if (two) d0[1] = o01;
+                  dst.one(d0, o00);
+                  if (two) dst.one(d0 + 1, o01);
                 }
               }
               if (r0 + 1 < oh) {
-                float* d1 = at32(dst, (unsigned)((r0 + 1) * ow + ucol));
+                const unsigned d1 = (unsigned)((r0 + 1) * ow + ucol);
                 if (pair) {
-                  *reinterpret_cast<float2*>(d1) = make_float2(o10, o11);
+                  dst.pair(d1, o10, o11);
                 } else {
-                  d1[0] = o10;
-                  if (two) d1[1] = o11;
+                  dst.one(d1, o10);
+                  if (two) dst.one(d1 + 1, o11);
                 }
               }
             }
@@ -397,5 +428,14 @@ __device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float s
   }
 }
 
+template <int L, int PF = kSynPF, bool PK = (L >= 12)>
+__device__ __forceinline__ void syn_stream(const float* __restrict__ pA, float sa, const float* __restrict__ pH,
+                                           const float* __restrict__ pV, const float* __restrict__ pD, float sd,
+                                           int mh, int mw, float* __restrict__ dst, int oh, int ow, int strip,
+                                           int qbeg, int qend, float4* xch, const float (&rlo)[L],
+                                           const float (&rhi)[L], int lane, bool vec2 = true) {
+  syn_stream_to<L, PF, PK>(pA, sa, pH, pV, pD, sd, mh, mw, SynOutF32{dst}, oh, ow, strip, qbeg, qend, xch, rlo, rhi,
+                           lane, vec2);
+}
 
 }  // namespace wam_rows

@@ -20,6 +20,7 @@ holds the single-process gradient.
 import collections
 import contextlib
 import math
+import os
 
 import numpy as np
 import torch
@@ -83,13 +84,18 @@ def trainable_params(model):
 
 
 def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=False, y_none_mean=False,
-                   input_dtype=None, batch=None, params=None, out=None):
+                   input_dtype=None, batch=None, params=None, out=None, native=False):
     """Gradient of the summed per-group reference losses w.r.t. img (fp32, contiguous; written into
     `out` when given). params (default: the model's parameters that require grad): their gradients
     are accumulated into .grad, as the reference's loss.backward() does. The gradient is taken
     w.r.t. the tensor the model is fed (bf16 and / or channels_last) and converted to img's dtype
     and layout by ONE copy into the result -- autograd's cast and the layout copy were two more
-    passes over it; the values are the same (the bf16 -> fp32 cast is exact)."""
+    passes over it; the values are the same (the bf16 -> fp32 cast is exact).
+    native=True: img is already the fed tensor (e.g. bf16 channels_last from
+    wam_waverec_bf16_nhwc) and the gradient is returned in that dtype, in whichever dense layout
+    (NCHW or NHWC) the model's backward produced it, without any conversion pass, whenever no loss
+    scale has to be applied after the backward (power-of-two scales are seeded; otherwise the fp32
+    contiguous gradient is returned as without native)."""
     img = img.detach().requires_grad_(True)
     inp = img if input_dtype is None else img.to(input_dtype)
     inp = inp.contiguous(memory_format=torch.channels_last) if channels_last and img.dim() == 4 else inp
@@ -110,7 +116,13 @@ def input_gradient(model, img, y, groups, n, autocast_dtype=None, channels_last=
     if g is None:
         raise RuntimeError("the model's output does not depend on its input")
     with torch.no_grad():
-        if out is None and g.dtype == img.dtype and g.is_contiguous():
+        if native and out is None and scale is None and g.dtype == img.dtype and (
+                g.is_contiguous() or g.is_contiguous(memory_format=torch.channels_last)):
+            out = g  # the fed dtype, NCHW or NHWC: the maps pass reads either
+        elif native and out is None:  # a scale to apply: the fp32 contiguous gradient
+            out = torch.empty(img.shape, dtype=torch.float32, device=img.device)
+            out.copy_(g)
+        elif out is None and g.dtype == img.dtype and g.is_contiguous():
             out = g
         else:
             out = torch.empty(img.shape, dtype=img.dtype, device=img.device) if out is None else out
@@ -205,11 +217,17 @@ class GradModel:
         """The parameters whose .grad a call accumulates (none for the folded copy)."""
         return [] if self.optimize else trainable_params(self.model)
 
-    def __call__(self, img, y, groups, n, y_none_mean=False, batch=None, out=None):
+    @property
+    def feeds_bf16_nhwc(self):
+        """The model is fed bf16 channels_last images (the folded bf16 copy): the WAM path can hand
+        them over in that form (wam_waverec_bf16_nhwc) and take the gradient back in it."""
+        return self.optimize and self.autocast_dtype == torch.bfloat16 and self.channels_last
+
+    def __call__(self, img, y, groups, n, y_none_mean=False, batch=None, out=None, native=False):
         run = self._runner()
         if self.optimize:  # a folded copy: the user's parameters are not touched
             return input_gradient(run, img, y, groups, n, None, self.channels_last, y_none_mean,
-                                  input_dtype=self.autocast_dtype, batch=batch, params=[], out=out)
+                                  input_dtype=self.autocast_dtype, batch=batch, params=[], out=out, native=native)
         return input_gradient(run, img, y, groups, n, self.autocast_dtype, self.channels_last, y_none_mean,
                               batch=batch, out=out)
 
@@ -424,6 +442,8 @@ def wam_budget_bytes(device=None):
     passes (and with it the fp32 summation order of the trapezoid / frame sums) does not follow the
     caching allocator from call to call.
     Larger passes read the trapezoid accumulators and the synthesis details fewer times per call.
+    Ranks that share one device (LOCAL_WORLD_SIZE > device count, e.g. the one-GPU gloo rehearsals)
+    read its free memory before the others have allocated, so each claims its share of the half.
     BUDGET_BYTES overrides it."""
     if BUDGET_BYTES is not None:
         return int(BUDGET_BYTES)
@@ -434,10 +454,20 @@ def wam_budget_bytes(device=None):
             budget = min(max(total // 8, 8 << 30), 64 << 30)
             free, _ = torch.cuda.mem_get_info(device)
             free += torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
-            budget = min(budget, max(free // 2, 1 << 30))
+            budget = min(budget, max(free // (2 * ranks_per_device()), 1 << 30))
     except (RuntimeError, AssertionError, ValueError):
         pass
     return budget_tier(budget)
+
+
+def ranks_per_device():
+    """Local ranks sharing each visible device: ceil(LOCAL_WORLD_SIZE / device count), >= 1."""
+    try:
+        lws = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    except ValueError:
+        lws = 1
+    nd = torch.cuda.device_count() if torch.cuda.is_available() else 1
+    return max(1, -(-lws // max(1, nd)))
 
 
 def budget_tier(b):

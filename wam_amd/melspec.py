@@ -251,9 +251,8 @@ def device_objective(inv, B):
     def evaluate(x):
         xh_np[:] = x
         xd.view(-1).copy_(xh, non_blocking=True)
-        diff = torch.addmm(B64, inv.A64, xd, alpha=1.0, beta=-1.0)          # A x - B
-        torch.sum(diff * diff, out=od[:1].view(()))
-        od[:1].mul_(scale * 0.5)
+        diff = torch.mm(inv.A64, xd).sub_(B64)                              # A x - B
+        od[:1].copy_(torch.sum(diff * diff).view(1)).mul_(scale * 0.5)
         torch.mm(inv.A64t, diff, out=od[1:].view(F, T))
         od[1:].mul_(scale)
         oh.copy_(od, non_blocking=True)

@@ -1,6 +1,7 @@
 """Python side of the C-ABI: plans (cached per device) and thin typed wrappers of every entry
 point of include/wam_hip.h. torch allocates every device buffer; every call is asynchronous on
 torch's current stream of the tensor's device."""
+import collections
 import ctypes
 import threading
 
@@ -109,6 +110,20 @@ class Plan:
                               stream_of(flat.device)))
         return out
 
+    def waverec_bf16_nhwc(self, flat, batch, channels, alphas=None, out=None):
+        """flat band-major coefficients of `batch` planes (images x channels) -> the reconstruction as
+        bf16 images [n_alpha * batch / channels, channels, *rec_shape] in channels_last memory (the
+        explained model's input dtype and layout; RNE rounding, as torch's cast). WAM_CAP_BF16_NHWC."""
+        require_cuda(flat, "coefficients")
+        n_alpha = 1 if alphas is None else len(alphas)
+        a = None if alphas is None else (c_f32 * n_alpha)(*[float(np.float32(v)) for v in alphas])
+        if out is None:
+            out = torch.empty((n_alpha * batch // channels, channels) + self.rec_shape, dtype=torch.bfloat16,
+                              device=flat.device, memory_format=torch.channels_last)
+        check(lib.wam_waverec_bf16_nhwc(self._h, batch, ptr(flat.contiguous()), a, n_alpha, channels, ptr(out),
+                                        stream_of(flat.device)))
+        return out
+
     def adjoint(self, grad, out=None):
         """grad [batch, *rec_shape] -> band-major coefficient gradients (waverec's VJP)."""
         require_cuda(grad, "grad")
@@ -139,14 +154,30 @@ class Plan:
                                        ptr(ws), stream_of(x.device)))
         return out
 
-    def adjoint_maps(self, grad, groups, group_items, channels, full=False):
-        """waverec VJP fused with the channel-mean |.| epilogue -> (maps, band_max[, coeff grads])."""
-        require_cuda(grad, "grad")
-        grad = grad.contiguous()
+    def adjoint_maps(self, grad, groups, group_items, channels, full=False, maps=None, band_max=None):
+        """waverec VJP fused with the channel-mean |.| epilogue -> (maps, band_max[, coeff grads]).
+        grad: fp32 [images * channels, *rec_shape], or a bf16 channels_last [images, channels,
+        *rec_shape] tensor (the model's own gradient; WAM_CAP_BF16_NHWC, full=False). maps / band_max:
+        optional outputs (band_max zero-filled by the caller)."""
+        if grad.dtype == torch.bfloat16:
+            require_cuda(grad[:0].float(), "grad")  # the device check only
+        else:
+            require_cuda(grad, "grad")
         images = groups * group_items
         dev = grad.device
-        maps = torch.empty(images * self.coeff_numel, dtype=torch.float32, device=dev)
-        bmax = torch.zeros((groups, self.nbands), dtype=torch.float32, device=dev)
+        maps = torch.empty(images * self.coeff_numel, dtype=torch.float32, device=dev) if maps is None else maps
+        bmax = torch.zeros((groups, self.nbands), dtype=torch.float32, device=dev) if band_max is None else band_max
+        if grad.dtype == torch.bfloat16:
+            if full or grad.dim() != 4:
+                raise ValueError("bf16 input gradients: an [images, channels, H, W] tensor, full=False")
+            nhwc = grad.is_contiguous(memory_format=torch.channels_last)
+            if not (nhwc or grad.is_contiguous()):
+                grad = grad.contiguous(memory_format=torch.channels_last)
+                nhwc = True
+            check(lib.wam_waverec_adjoint_maps_bf16(self._h, groups, group_items, channels, int(nhwc), ptr(grad),
+                                                    ptr(maps), ptr(bmax), stream_of(dev)))
+            return maps, bmax, None
+        grad = grad.contiguous()
         cg = torch.empty(images * channels * self.coeff_numel, dtype=torch.float32, device=dev) if full else None
         ws = self.workspace(images * channels)
         check(lib.wam_waverec_adjoint_maps(self._h, groups, group_items, channels, ptr(grad), ptr(maps), ptr(bmax),
@@ -175,6 +206,7 @@ PLAN_NO_COOP = 8
 PLAN_FORCE_COOP = 16
 CAP_NOISY_WAVEDEC = 1
 CAP_ADJOINT_MAPS = 2
+CAP_BF16_NHWC = 4
 
 
 def timing_enable(on=True):
@@ -197,9 +229,11 @@ def timing_drain():
 
 
 # -------------------------------------------------------------------- WAM epilogue wrappers
-# (device, items, len) -> zero-initialised workspace of the split sigma reduction (its arrival
-# counters are reset by every call, so one buffer serves every call of that shape)
-_SIGMA_WS = {}
+# (device, stream, items, len) -> zero-initialised workspace of the split sigma reduction (its
+# arrival counters are reset by every call, so one buffer serves the calls of that shape issued in
+# order on one stream; calls on another stream get their own); least recently used entries go first
+_SIGMA_WS = collections.OrderedDict()
+_SIGMA_WS_MAX = 16
 
 
 def item_sigma(x, item_stride, length, spread):
@@ -209,13 +243,17 @@ def item_sigma(x, item_stride, length, spread):
     sigma = torch.empty(items, dtype=torch.float32, device=x.device)
     if items == 0:
         return sigma
-    key = (str(x.device), int(items), int(length))
+    st = stream_of(x.device)
+    key = (str(x.device), int(st.value or 0), int(items), int(length))
     ws = _SIGMA_WS.get(key)
     if ws is None:
         nb = int(lib.wam_item_sigma_ws_bytes(items, length))
         ws = _SIGMA_WS[key] = torch.zeros((nb + 7) // 8, dtype=torch.float64, device=x.device)
+        while len(_SIGMA_WS) > _SIGMA_WS_MAX:
+            _SIGMA_WS.popitem(last=False)
+    _SIGMA_WS.move_to_end(key)
     check(lib.wam_item_sigma_ws(items, item_stride, length, ptr(x), float(np.float32(spread)), ptr(sigma), ptr(ws),
-                                ws.numel() * 8, stream_of(x.device)))
+                                ws.numel() * 8, st))
     return sigma
 
 

@@ -25,6 +25,10 @@ Build-only keyword arguments (all optional, after the reference's own):
                  batch-global band maxima combined by an all-reduce MAX before normalising and the
                  rows gathered at the end; 'auto' (default) = 'images' when every rank gets an
                  image, else 'samples'.
+  bf16_handoff   True (default): with a bf16 channels_last folded model (optimize_model +
+                 autocast_dtype=torch.bfloat16 + channels_last) the SmoothGrad synthesis writes the
+                 model's input as bf16 NHWC and the maps pass reads its bf16 NHWC gradient (no
+                 cast / layout passes; the same values as the fp32 hand-off); False: fp32 hand-off.
 """
 import numpy as np
 import torch
@@ -35,7 +39,7 @@ from .profiling import phase
 from .constants import WaveletDetailTuple2d
 from .engine import (GradModel, LegacyNoise, Shard, auto_group, chunks, ig_weights, model_device, param_grad_sum,
                      require_gpu_device, wam_budget_bytes, wam_group)
-from .plan import (CAP_ADJOINT_MAPS, CAP_NOISY_WAVEDEC, disentangle_scales, frame_accumulate, frame_trapz,
+from .plan import (CAP_ADJOINT_MAPS, CAP_BF16_NHWC, CAP_NOISY_WAVEDEC, disentangle_scales, frame_accumulate, frame_trapz,
                    get_plan, item_sigma, noise_add, reproject_scales, subband_maps)
 
 
@@ -153,12 +157,20 @@ class BaseWAM2D:
     def wavelet_coeffs(self, v):
         self._wavelet_coeffs = v
 
+    @staticmethod
+    def _planes(plan, gimg, n, c):
+        """A recorded input gradient as fp32 planes [n * c, *rec] (a bf16 channels_last gradient of
+        the model hand-off widened: exact)."""
+        if gimg.dtype != torch.float32:
+            gimg = gimg.float().contiguous()
+        return gimg.reshape((n * c,) + tuple(plan.rec_shape))
+
     @property
     def gradient_coeffs(self):
         if self._gradient_coeffs is None and self._pass is not None:
             plan, _, (gf, b, f), n, c, gimg = self._pass
             if gimg is not None:
-                gf, b, f = plan.adjoint(gimg), n * c, 0
+                gf, b, f = plan.adjoint(self._planes(plan, gimg, n, c)), n * c, 0
             self._gradient_coeffs = _to_numpy_2d(plan, gf, b, n, c, f)
         return self._gradient_coeffs
 
@@ -177,7 +189,7 @@ class BaseWAM2D:
         mean| maps + batch maxima (wam_subband_maps) -> bilinear reprojection (k_disentangle)."""
         plan, _, (gf, b, f), n, c, gimg = self._pass
         if gimg is not None:
-            gf, b, f = plan.adjoint(gimg), n * c, 0
+            gf, b, f = plan.adjoint(self._planes(plan, gimg, n, c)), n * c, 0
         views = plan.split(gf, b)
         cg = torch.cat([v[f * c:(f + n) * c].reshape(-1) for v in views])  # this pass's n*c items
         maps, bmax = subband_maps(plan, cg, 1, n, c)
@@ -292,7 +304,7 @@ class WaveletAttribution2D(BaseWAM2D):
     def __init__(self, model, wavelet="haar", method="smooth", J=3, device=None, mode="reflect", approx_coeffs=False,
                  normalize_coeffs=True, n_samples=25, stdev_spread=0.25, random_seed=42, *, noise="numpy",
                  frame="legacy", sample_batch=None, autocast_dtype=None, channels_last=False, dist=None,
-                 optimize_model=False, dist_axis="auto"):
+                 optimize_model=False, dist_axis="auto", bf16_handoff=True):
         super().__init__(model, wavelet=wavelet, J=J, device=device, mode=mode, approx_coeffs=approx_coeffs,
                          normalize_coeffs=normalize_coeffs, frame=frame, autocast_dtype=autocast_dtype,
                          channels_last=channels_last, optimize_model=optimize_model)
@@ -308,6 +320,9 @@ class WaveletAttribution2D(BaseWAM2D):
         if dist_axis not in ("auto", "samples", "images"):
             raise ValueError("dist_axis must be 'auto', 'samples' or 'images'")
         self.dist_axis = dist_axis
+        # a bf16 channels_last model gets its input from the synthesis in that form and hands its
+        # gradient to the maps pass in it (no cast / layout passes); False: the fp32 hand-off
+        self.bf16_handoff = bool(bf16_handoff)
         self.wam = BaseWAM2D(model, wavelet=wavelet, J=J, mode=mode, device=device, approx_coeffs=approx_coeffs,
                              normalize_coeffs=normalize_coeffs, frame=frame, autocast_dtype=autocast_dtype,
                              channels_last=channels_last, _grad=self._grad)
@@ -382,6 +397,26 @@ class WaveletAttribution2D(BaseWAM2D):
             return shard, axis, shard.range(n), (0, n_steps)
         return shard, axis, (0, n), shard.range(n_steps)
 
+    def _handoff_groups(self, plan, img, y, cnt, n, c, group, batch):
+        """Model input gradients and WAM maps of `cnt` samples whose reconstruction img is bf16
+        channels_last [cnt * n, c, *rec] (wam_waverec_bf16_nhwc), one model group at a time: each
+        group's bf16 gradient goes straight into the maps pass (wam_waverec_adjoint_maps_bf16_nhwc,
+        widened on load: the maps equal the fp32 path's bit for bit) and its rows of maps / band_max.
+        -> (maps, band_max, the last sample's input gradient)."""
+        K = plan.coeff_numel
+        maps = torch.empty(cnt * n * K, dtype=torch.float32, device=img.device)
+        bmax = torch.zeros((cnt, plan.nbands), dtype=torch.float32, device=img.device)
+        gk = None
+        for g0, gc in chunks(0, cnt, group):
+            with phase("model"):
+                gk = self._grad(img[g0 * n:(g0 + gc) * n], y, gc, n, batch=batch, native=True)
+            with phase("adjoint+maps"):
+                if gk.dtype != torch.bfloat16:  # a loss scale was applied in fp32
+                    gk = gk.reshape((gc * n * c,) + tuple(plan.rec_shape))
+                plan.adjoint_maps(gk, gc, n, c, maps=maps[g0 * n * K:(g0 + gc) * n * K], band_max=bmax[g0:g0 + gc])
+        last = gk[-n:] if gk.dim() == 4 else gk[-n * c:]
+        return maps, bmax, last
+
     def smooth_gradcam(self, x, y):
         """lib/wam_2D.py:379-415."""
         dev = self._dev
@@ -402,6 +437,8 @@ class WaveletAttribution2D(BaseWAM2D):
         # parity mode streams the host-generated legacy noise one model group at a time
         wgroup = group if self.noise == "numpy" else self._wam_group(plan, n_ref, c, group, s_hi - s_lo, shard, axis)
         frame = torch.zeros(n * rh * rw, dtype=torch.float64, device=dev)
+        handoff = (self._grad.feeds_bf16_nhwc and c in (1, 3) and bool(plan.caps & CAP_BF16_NHWC)
+                   and self.bf16_handoff)
         legacy = None
         if self.noise == "numpy":
             legacy = LegacyNoise(sigma_all.cpu().numpy(), (c, h, w), self.random_seed, self.n_samples, dev)
@@ -419,12 +456,20 @@ class WaveletAttribution2D(BaseWAM2D):
                         noisy = noise_add(xs, sigma, cnt, n, item, item, seed=self.random_seed, sample_base=s0,
                                           item_base=i_lo)
                         flat = plan.wavedec(noisy.view(cnt * n * c, h, w))
-                with phase("waverec2"):
-                    img = plan.waverec(flat, cnt * n * c)[0].view((cnt * n, c) + rec)
-                with phase("model"):
-                    g = self._gradients(img, y, cnt, n, group, batch)
-                with phase("adjoint+maps"):
-                    maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
+                if handoff:
+                    # the model's own dtype and layout across the boundary: bf16 NHWC reconstruction
+                    # in, bf16 NHWC gradient out, maps per model group straight from it
+                    with phase("waverec2"):
+                        img = plan.waverec_bf16_nhwc(flat, cnt * n * c, c)
+                    maps, bmax, last_g = self._handoff_groups(plan, img, y, cnt, n, c, group, batch)
+                else:
+                    with phase("waverec2"):
+                        img = plan.waverec(flat, cnt * n * c)[0].view((cnt * n, c) + rec)
+                    with phase("model"):
+                        g = self._gradients(img, y, cnt, n, group, batch)
+                    with phase("adjoint+maps"):
+                        maps, bmax, _ = self._adjoint_maps(plan, g.view((cnt * n * c,) + rec), cnt, n, c, full=False)
+                    last_g = g[(cnt - 1) * n:].reshape((n * c,) + rec)
                 if axis == "images":
                     with phase("all_reduce_max"):
                         shard.all_reduce_max(bmax)  # per-sample maxima over the whole batch (A.6)
@@ -432,7 +477,6 @@ class WaveletAttribution2D(BaseWAM2D):
                     frame_accumulate(cnt, n, gmap, maps, plan.coeff_numel, bmax, plan.nbands, self.normalize_coeffs,
                                      frame)
                 last = (plan, flat, None, cnt * n * c, (cnt - 1) * n, n, c)
-                last_g = g[(cnt - 1) * n:].reshape((n * c,) + rec)
         if legacy is not None:
             legacy.finish()
         if last is not None:
