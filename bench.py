@@ -184,6 +184,11 @@ def parse(argv=None):
     ap.add_argument("--dist-axis", default=None, choices=["auto", "samples", "images"])
     ap.add_argument("--dist-timeout", type=float, default=300.0,
                     help="seconds a collective may wait before the rank aborts (N > 1)")
+    ap.add_argument("--rank-slice", default=None, metavar="N[,N...]",
+                    help="one GPU: time the slice ONE rank of an N-GPU run would process, on the images and the "
+                         "samples axis, and print the projected strong-scaling efficiency per N (no bench line)")
+    ap.add_argument("--link-GBps", type=float, default=50.0,
+                    help="--rank-slice: bus bandwidth assumed for the collectives' projection")
     ap.add_argument("--wam-probe", action="store_true", help=argparse.SUPPRESS)  # PMC child run
     # test-only: the process group's backend and every rank on cuda:0 (rehearsing the N > 1 path on
     # a one-GPU box); the driver's runs use the defaults (RCCL, one GPU per rank)
@@ -740,12 +745,93 @@ def collectives_timing(wl, dev, world, axis):
     return out
 
 
+# ============================================================================ rank-slice projection
+def _slice_workload(wl, n_img, n_steps):
+    """wl restricted to its first n_img items and n_steps noise samples / IG steps."""
+    import copy
+    w = copy.copy(wl)
+    w.n, w.n_steps = n_img, n_steps
+    w.kw = dict(wl.kw, n_samples=n_steps)
+    return w
+
+
+def _collective_bytes(wl, axis, world):
+    """Bytes each rank's collectives move per call (ring algorithms: all-gather (N-1)/N of the
+    whole, all-reduce 2 (N-1)/N), the sizes of collectives_timing / DESIGN.md section 6."""
+    f = (world - 1) / world
+    if axis == "images":
+        H = 224 if wl.name != "c4" else 512
+        rows = -(-wl.n // world) * world * H * H * 8           # fp64 frame rows, all-gathered
+        return f * rows + 2 * f * wl.n_steps * (3 * wl.kw["J"] + 1) * 4
+    if wl.dim == 1:
+        numel = wl.n * (80052 + 157 * 128)
+        return 2 * f * numel * 4
+    if wl.dim == 3:
+        return 2 * f * wl.n * 128 ** 3 * 4
+    if wl.name == "c4":
+        return 2 * f * wl.n * 512 * 512 * 4
+    return 2 * f * wl.n * 224 * 224 * 8
+
+
+def rank_slice(args, wl):
+    """Single-GPU strong-scaling projection: for every N the slice the busiest
+    rank processes -- images axis: ceil(n / N) items x all samples; samples axis: all items x
+    ceil(S / N) samples -- timed alone on this GPU with its own model batch; projected N-GPU step =
+    slice time + the collectives' bytes at --link-GBps; efficiency = T_1 / (N * T_N)."""
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    import wam_amd  # noqa: F401
+    x, y = wl.make_x(), (wl.make_y() if wl.make_y else None)
+    xd = x.to(dev)
+    steps, warm = args.steps, args.warmup
+
+    def run(w, n_img):
+        ex = build_explainer(w, dev, args, n_local=n_img)
+        yy = y[:n_img] if isinstance(y, list) else y
+        dt, _, _ = timed(lambda: ex(xd[:n_img], yy), steps, warm, 1, dev)
+        sb = getattr(ex, "sample_batch", None)
+        del ex
+        torch.cuda.empty_cache()
+        return dt / steps, sb
+
+    t1, sb1 = run(wl, wl.n)
+    rows = []
+    axes = ["images", "samples"] if wl.dim == 2 else ["samples"]
+    for N in [int(v) for v in args.rank_slice.split(",")]:
+        for axis in axes:
+            if axis == "images":
+                w = _slice_workload(wl, -(-wl.n // N), wl.n_steps)
+            else:
+                w = _slice_workload(wl, wl.n, -(-wl.n_steps // N))
+            log("rank slice N=%d %s axis: %d items x %d samples" % (N, axis, w.n, w.n_steps))
+            ts, sb = run(w, w.n)
+            cb = _collective_bytes(wl, axis, N)
+            tc = cb / (args.link_GBps * 1e9)
+            tn = ts + tc
+            rows.append({"n_gpus": N, "axis": axis, "slice_items": w.n, "slice_samples": w.n_steps,
+                         "model_batch": (sb or 0) * w.n, "slice_ms": round(ts * 1e3, 2),
+                         "collective_MB": round(cb / 1e6, 2), "collective_ms_model": round(tc * 1e3, 3),
+                         "projected_value": round(wl.n / tn, 3),
+                         "projected_efficiency": round(t1 / (N * tn), 4)})
+    best = {}
+    for r in rows:
+        if r["n_gpus"] not in best or r["projected_value"] > best[r["n_gpus"]]["projected_value"]:
+            best[r["n_gpus"]] = r
+    print(json.dumps({"config": wl.name, "metric": wl.metric, "one_gpu": {"ms_per_step": round(t1 * 1e3, 2),
+                      "value": round(wl.n / t1, 3), "model_batch": (sb1 or 0) * wl.n},
+                      "link_GBps_assumed": args.link_GBps, "steps": steps, "warmup": warm, "slices": rows,
+                      "best_axis": {str(k): v["axis"] for k, v in sorted(best.items())}}))
+    return 0
+
+
 # ============================================================================ main
 def main():
     args = parse()
     if args.wam_probe:
         return wam_probe(args)
     heartbeat()
+    if args.rank_slice:
+        return rank_slice(args, workload(args.config))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return self_launch(args, sys.argv[1:])
     world = int(os.environ.get("WORLD_SIZE", "1"))
