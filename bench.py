@@ -221,7 +221,7 @@ def self_launch(args, argv):
 
 # ============================================================================ explainer
 def build_explainer(wl, dev, args, model=None, dist_on=False, model_dtype=None, optimize=None, noise=None,
-                    n_local=None):
+                    n_local=None, axis=None):
     import wam_amd
     model_dtype = model_dtype or args.model_dtype or wl.model_dtype
     model = (model if model is not None else wl.model()).to(dev).eval()
@@ -240,7 +240,7 @@ def build_explainer(wl, dev, args, model=None, dist_on=False, model_dtype=None, 
         sb = args.sample_batch or _auto_sample_batch(wl, n_local or wl.n)
         return wam_amd.WaveletAttribution2D(model, sample_batch=sb, autocast_dtype=ac, channels_last=cl,
                                             optimize_model=opt, dist=True if dist_on else None,
-                                            dist_axis=args.dist_axis or wl.dist_axis,
+                                            dist_axis=axis or args.dist_axis or wl.dist_axis,
                                             bf16_handoff=not args.no_bf16_handoff, **kw)
     if wl.dim == 1:
         return wam_amd.WaveletAttribution1D(model, sample_batch=args.sample_batch or 5, autocast_dtype=ac,
@@ -745,6 +745,13 @@ def collectives_timing(wl, dev, world, axis):
     return out
 
 
+# The sharding axis per (config, world size) that the single-GPU rank-slice projection measured
+# faster (bench.py --rank-slice); other N use the config's default axis
+MEASURED_AXIS = {
+    "c2": {2: "samples", 4: "images", 8: "images"},   # profiles/r06e_rank_slice_c2.log
+}
+
+
 # ============================================================================ rank-slice projection
 def _slice_workload(wl, n_img, n_steps):
     """wl restricted to its first n_img items and n_steps noise samples / IG steps."""
@@ -866,7 +873,7 @@ def main():
             y = int(wl.model()(x).argmax().item())
     xd = x.to(dev)
     shard_on = world > 1
-    axis = args.dist_axis or wl.dist_axis
+    axis = args.dist_axis or MEASURED_AXIS.get(wl.name, {}).get(world) or wl.dist_axis
     if wl.dim != 2 or axis == "auto":
         axis = "images" if (wl.dim == 2 and wl.n >= world) else "samples"
     n_local, s_local = wl.n, wl.n_steps
@@ -877,7 +884,8 @@ def main():
         else:
             s_local = hi - lo
     # the sample batch is sized from the largest rank's image count, the same on every rank
-    ex = build_explainer(wl, dev, args, dist_on=shard_on, n_local=-(-wl.n // world) if axis == "images" else wl.n)
+    ex = build_explainer(wl, dev, args, dist_on=shard_on, n_local=-(-wl.n // world) if axis == "images" else wl.n,
+                         axis=axis)
     log("%s: %d warm-up + %d timed steps on %d GPU(s)" % (wl.name, args.warmup, args.steps, world))
     dt, records, out = timed(lambda: ex(xd, y), args.steps, args.warmup, world, dev)
     assert out is not None

@@ -693,24 +693,15 @@ __global__ void __launch_bounds__(256) k_disentangle(int64_t items, int size, in
 }
 
 
-// Streaming copy: the measured HBM ceiling bench.py reports beside the 8 TB/s spec peak. Each
-// thread keeps kCopyU 16-B loads in flight (all issued before the first store) and walks the
-// buffer in grid-sized strides of kCopyU * blockDim float4 per block; nontemporal loads / stores
-// (streamed once, no reuse).
-constexpr int kCopyU = 4;
+// Streaming copy: the measured HBM ceiling bench.py reports beside the 8 TB/s spec peak. One 16-B
+// load and store per thread over a grid covering the buffer once (no grid-stride loop): the fastest
+// of the forms swept by scripts/ubench_copy.hip on MI355X (6.17 TB/s for a 2 GiB copy against
+// 5.28 TB/s for the round-5 grid-stride nontemporal form with 4 loads in flight per thread,
+// profiles/r06e_ubench_copy.log); buffers past 2^31 blocks take the grid-stride loop.
 typedef float wam_f4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(256) k_copy(int64_t n4, const wam_f4* __restrict__ src, wam_f4* __restrict__ dst) {
-  const int64_t step = (int64_t)gridDim.x * blockDim.x * kCopyU;
-  int64_t t = (int64_t)blockIdx.x * blockDim.x * kCopyU + threadIdx.x;
-  for (; t + (kCopyU - 1) * (int64_t)blockDim.x < n4; t += step) {
-    wam_f4 v[kCopyU];
-#pragma unroll
-    for (int u = 0; u < kCopyU; ++u) v[u] = __builtin_nontemporal_load(src + t + u * (int64_t)blockDim.x);
-#pragma unroll
-    for (int u = 0; u < kCopyU; ++u) __builtin_nontemporal_store(v[u], dst + t + u * (int64_t)blockDim.x);
-  }
-  for (int u = 0; u < kCopyU; ++u, t += blockDim.x)  // the tail (< kCopyU * blockDim per block)
-    if (t < n4) dst[t] = src[t];
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += step) dst[t] = src[t];
 }
 
 }  // namespace
@@ -981,8 +972,7 @@ int wam_copy(int64_t bytes, const void* src, void* dst, void* stream) {
   const int64_t n4 = bytes / 16;
   if (n4 == 0) return WAM_OK;
   WamTimer tm((hipStream_t)stream, "k_copy", 2.0 * bytes);
-  hipLaunchKernelGGL(k_copy, dim3(wam_grid((n4 + kCopyU - 1) / kCopyU, 256, 256 * 32)), dim3(256), 0,
-                     (hipStream_t)stream, n4,
+  hipLaunchKernelGGL(k_copy, dim3(wam_grid(n4, 256, int64_t(1) << 31)), dim3(256), 0, (hipStream_t)stream, n4,
                      (const wam_f4*)src, (wam_f4*)dst);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
