@@ -280,9 +280,11 @@ def unit_bytes(wl, kname, units_per_launch, lib_bytes, n_items):
     A kernel that covers only part of each item (the 1D interior / boundary tiles) keeps its share:
     the library's bytes over the whole-item library count."""
     from wam_amd import plan as P
-    if wl.name == "c2" and kname in ("k_plane_syn", "k_plane_maps"):
+    if wl.name == "c2" and kname.split("<")[0] in ("k_plane_syn", "k_plane_maps"):
         K = P.get_plan(2, (224, 224), 3, "db4", "reflect", "cuda").coeff_numel
-        per_unit = {"k_plane_syn": 4 * 3 * (K + 224 * 224), "k_plane_maps": 4 * (3 * 224 * 224 + K)}[kname]
+        px = 2 if "bf16" in kname else 4  # the bf16 hand-off forms move 2 B per pixel
+        per_unit = {"k_plane_syn": 3 * (4 * K + px * 224 * 224),
+                    "k_plane_maps": px * 3 * 224 * 224 + 4 * K}[kname.split("<")[0]]
         return per_unit * units_per_launch
     if not kname.endswith("<noise>"):
         return None
@@ -428,12 +430,12 @@ def _short_kernel(name):
     return short(name)
 
 
-def _pmc_pass(counter, config, outdir):
+def _pmc_pass(counter, config, outdir, extra=()):
     exe = shutil.which("rocprofv3")
     log("rocprofv3 --pmc %s pass (child run of %s)" % (counter, config))
     cmd = ["timeout", "-s", "KILL", "150", exe, "--pmc", counter, "--kernel-include-regex", "k_[a-z0-9_]+",
            "--output-format", "csv", "-d", outdir, "-o", "run", "--", sys.executable, os.path.join(REPO, "bench.py"),
-           "--config", config, "--wam-probe"]
+           "--config", config, "--wam-probe"] + list(extra)
     env = dict(os.environ, TMPDIR="/tmp")
     p = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=200)
     files = glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True)
@@ -455,7 +457,7 @@ def _pmc_pass(counter, config, outdir):
     return {k: (len(v), sum(v.values())) for k, v in acc.items()}
 
 
-def live_pmc(config):
+def live_pmc(config, extra=()):
     """HBM traffic per WAM-kernel launch: two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; they
     do not fit one pass) over one call of this config with a stand-in model, started before this
     process touches the GPU. FETCH_SIZE is doubled (gfx950 counts 16-B-per-lane streaming reads at
@@ -464,8 +466,8 @@ def live_pmc(config):
         return None
     tmp = tempfile.mkdtemp(prefix="wam_pmc_", dir="/tmp")
     try:
-        fetch = _pmc_pass("FETCH_SIZE", config, os.path.join(tmp, "f"))
-        write = _pmc_pass("WRITE_SIZE", config, os.path.join(tmp, "w"))
+        fetch = _pmc_pass("FETCH_SIZE", config, os.path.join(tmp, "f"), extra)
+        write = _pmc_pass("WRITE_SIZE", config, os.path.join(tmp, "w"), extra)
     except Exception as e:  # profiler unavailable / refused: report null traffic, say why
         return {"error": str(e)[:400]}
     finally:
@@ -500,7 +502,10 @@ def wam_probe(args):
     dev = torch.device("cuda", 0)
     x, y = wl.make_x(), (wl.make_y() if wl.make_y else 0)
     model = _StandIn(wl.dim, 1000 if wl.dim == 2 else 50)
-    ex = build_explainer(wl, dev, args, model=model, model_dtype="fp32", optimize=False)
+    if wl.name == "c2":  # the headline's model precision and execution: the bf16 NHWC hand-off kernels
+        ex = build_explainer(wl, dev, args, model=model)
+    else:
+        ex = build_explainer(wl, dev, args, model=model, model_dtype="fp32", optimize=False)
     ex(x.to(dev), y)
     torch.cuda.synchronize()
 
@@ -851,7 +856,8 @@ def main():
     wl = workload(args.config)
     traffic = None
     if rank == 0 and world == 1 and args.pmc == "auto":
-        traffic = live_pmc(args.config)  # child processes, BEFORE this process touches the GPU
+        # child processes, BEFORE this process touches the GPU
+        traffic = live_pmc(args.config, ["--no-bf16-handoff"] if args.no_bf16_handoff else [])
     if world > 1:
         torch.cuda.set_device(local)
         # a collective that does not complete within the timeout aborts the rank with the

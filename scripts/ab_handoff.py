@@ -1,7 +1,8 @@
 """Same-process A/B of the c2 model hand-off: the bf16 NHWC hand-off
 (bf16_handoff=True: k_plane_syn writes the model input as bf16 NHWC, the maps pass reads the model's
 bf16 gradient) against the fp32 hand-off (cast / layout passes) on one box, in one process,
-alternating rounds so that the bf16 model's run-to-run drift hits both sides alike.
+alternating rounds so that the bf16 model's run-to-run drift hits both sides alike; a third arm
+runs the hand-off maps of model group k on a side stream beside group k+1's model pass.
 
 usage: python scripts/ab_handoff.py [--rounds 6] [--steps 5]
 """
@@ -26,9 +27,11 @@ def main():
     wl = bench.workload("c2")
     x, y = wl.make_x().to(dev), wl.make_y()
     exs = {}
-    for tag, off in (("bf16_handoff", False), ("fp32_handoff", True)):
+    for tag, off, side in (("bf16_handoff", False, False), ("fp32_handoff", True, False),
+                           ("bf16_sidestream", False, True)):
         args = bench.parse(["--config", "c2"] + (["--no-bf16-handoff"] if off else []))
         exs[tag] = bench.build_explainer(wl, dev, args, n_local=wl.n)
+        exs[tag].maps_side_stream = side
         for _ in range(2):
             exs[tag](x, y)
     torch.cuda.synchronize()
@@ -42,10 +45,10 @@ def main():
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) / a.steps * 1e3
             res[tag].append(ms)
-            print("round %d %-13s %8.2f ms per step" % (r, tag, ms), flush=True)
+            print("round %d %-15s %8.2f ms per step" % (r, tag, ms), flush=True)
     for tag, v in res.items():
         v = sorted(v)
-        print("%-13s median %.2f  min %.2f  max %.2f ms per step" % (tag, v[len(v) // 2], v[0], v[-1]))
+        print("%-15s median %.2f  min %.2f  max %.2f ms per step" % (tag, v[len(v) // 2], v[0], v[-1]))
 
 
 if __name__ == "__main__":

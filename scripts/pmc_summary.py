@@ -22,10 +22,13 @@ def short(name):
     args = [a.strip() for a in m.group(3).split(",")] if m.group(3) else []
     if base in ("k_ana_rows", "k_haar3_ana", "k_dwt1_ana", "k_dwt1_ana_p", "k_dwt1_ana_int") and args and args[-1] == "true":
         return base + "<noise>"
-    if base == "k_plane_ana" and len(args) >= 5:  # <L, CPL, NOISE, MC, MAPS>
+    if base == "k_plane_ana" and len(args) >= 5:  # <L, CPL, NOISE, MC, MAPS, COOP, IN>
         if args[4] == "true":
-            return "k_plane_maps"
+            fmt = args[6] if len(args) >= 7 else "0"
+            return {"1": "k_plane_maps<bf16nhwc>", "2": "k_plane_maps<bf16>"}.get(fmt, "k_plane_maps")
         return "k_plane_ana<noise>" if args[2] == "true" else "k_plane_ana"
+    if base == "k_plane_syn" and len(args) >= 2 and args[1] != "0":  # <L, OC>: bf16 NHWC output
+        return "k_plane_syn<bf16nhwc>"
     return base
 
 

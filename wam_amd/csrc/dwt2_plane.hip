@@ -1206,7 +1206,7 @@ int launch_syn_plane_t(const SynGeom& g, int lds_bytes, int64_t n_items, const f
                                       kPlaneLdsCap));
     attr_set.fetch_or(bit);
   }
-  WamTimer tm(st, "k_plane_syn", bytes);
+  WamTimer tm(st, OC ? "k_plane_syn<bf16nhwc>" : "k_plane_syn", bytes);
   hipLaunchKernelGGL(kern, dim3((unsigned)n_items), dim3(kPT), lds_bytes, st, coeffs, out, filt, g, al, n_items);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
