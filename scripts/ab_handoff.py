@@ -1,8 +1,9 @@
 """Same-process A/B of the c2 model hand-off: the bf16 NHWC hand-off
 (bf16_handoff=True: k_plane_syn writes the model input as bf16 NHWC, the maps pass reads the model's
 bf16 gradient) against the fp32 hand-off (cast / layout passes) on one box, in one process,
-alternating rounds so that the bf16 model's run-to-run drift hits both sides alike; a third arm
-runs the hand-off maps of model group k on a side stream beside group k+1's model pass.
+alternating rounds so that the bf16 model's run-to-run drift hits both sides alike. (A third arm,
+the hand-off maps of model group k on a side stream beside group k+1's model pass, measured no gain
+and was removed: profiles/r06g_ab_handoff.log.)
 
 usage: python scripts/ab_handoff.py [--rounds 6] [--steps 5]
 """
@@ -27,11 +28,9 @@ def main():
     wl = bench.workload("c2")
     x, y = wl.make_x().to(dev), wl.make_y()
     exs = {}
-    for tag, off, side in (("bf16_handoff", False, False), ("fp32_handoff", True, False),
-                           ("bf16_sidestream", False, True)):
+    for tag, off in (("bf16_handoff", False), ("fp32_handoff", True)):
         args = bench.parse(["--config", "c2"] + (["--no-bf16-handoff"] if off else []))
         exs[tag] = bench.build_explainer(wl, dev, args, n_local=wl.n)
-        exs[tag].maps_side_stream = side
         for _ in range(2):
             exs[tag](x, y)
     torch.cuda.synchronize()

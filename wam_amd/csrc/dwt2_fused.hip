@@ -157,8 +157,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L <= 1
   const int qbeg = qs + chunk * RQ;
   const int qend = min(qbeg + RQ, qlast + 1);
   const int64_t in_plane = (int64_t)mh * mw;
-  // long filters prefetch 2 rows ahead: 4 would cost the L = 16 kernel 3 waves per SIMD
-  wam_rows::syn_stream<L, (L >= 12 ? 2 : 4)>(A + plane * in_plane, sa, Hh + plane * in_plane, Vv + plane * in_plane, Dd + plane * in_plane,
+  // long filters prefetch 3 rows ahead: at 2 the L = 14 / 16 kernels kept 4-5 VGPRs in scratch (128
+  // VGPRs, ROCm 7.2), at 3 they need 110 / 122 and none (c4 level 0 at 8 alphas 1,491 -> 1,394 us,
+  // profiles/r06h_kc4_*.log); 4 would cost the L = 16 kernel 3 waves per SIMD
+  wam_rows::syn_stream<L, (L >= 12 ? 3 : 4)>(A + plane * in_plane, sa, Hh + plane * in_plane, Vv + plane * in_plane, Dd + plane * in_plane,
                           sd, mh, mw, out + plane * (int64_t)nh * nw, nh, nw, strip, qbeg, qend, xch[wv], rlo, rhi,
                           lane, (nw & 1) == 0);
 }

@@ -30,8 +30,6 @@ Build-only keyword arguments (all optional, after the reference's own):
                  model's input as bf16 NHWC and the maps pass reads its bf16 NHWC gradient (no
                  cast / layout passes; the same values as the fp32 hand-off); False: fp32 hand-off.
 """
-import os
-
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -90,16 +88,6 @@ def _reproject_wam(coeffs, normalize_coeffs):
         vis[:, s:e, :s] = vt[:, :(e - s), :(e - s)]
         vis[:, :s, s:e] = hz[:, :(e - s), :(e - s)]
     return vis
-
-
-_SIDE = {}
-
-
-def _side_stream(device):
-    """One side stream per device for WAM work overlapped with the model (maps_side_stream)."""
-    if device not in _SIDE:
-        _SIDE[device] = torch.cuda.Stream(device)
-    return _SIDE[device]
 
 
 def _bilinear_np(a, size):
@@ -335,8 +323,6 @@ class WaveletAttribution2D(BaseWAM2D):
         # a bf16 channels_last model gets its input from the synthesis in that form and hands its
         # gradient to the maps pass in it (no cast / layout passes); False: the fp32 hand-off
         self.bf16_handoff = bool(bf16_handoff)
-        # hand-off maps of model group k on a side stream beside group k+1's model pass (A/B switch)
-        self.maps_side_stream = os.environ.get("WAM_MAPS_SIDE_STREAM", "0") == "1"
         self.wam = BaseWAM2D(model, wavelet=wavelet, J=J, mode=mode, device=device, approx_coeffs=approx_coeffs,
                              normalize_coeffs=normalize_coeffs, frame=frame, autocast_dtype=autocast_dtype,
                              channels_last=channels_last, _grad=self._grad)
@@ -421,25 +407,13 @@ class WaveletAttribution2D(BaseWAM2D):
         maps = torch.empty(cnt * n * K, dtype=torch.float32, device=img.device)
         bmax = torch.zeros((cnt, plan.nbands), dtype=torch.float32, device=img.device)
         gk = None
-        main = torch.cuda.current_stream(img.device)
-        side = _side_stream(img.device) if self.maps_side_stream else None
         for g0, gc in chunks(0, cnt, group):
             with phase("model"):
                 gk = self._grad(img[g0 * n:(g0 + gc) * n], y, gc, n, batch=batch, native=True)
             with phase("adjoint+maps"):
                 if gk.dtype != torch.bfloat16:  # a loss scale was applied in fp32
                     gk = gk.reshape((gc * n * c,) + tuple(plan.rec_shape))
-                if side is None:
-                    plan.adjoint_maps(gk, gc, n, c, maps=maps[g0 * n * K:(g0 + gc) * n * K],
-                                      band_max=bmax[g0:g0 + gc])
-                else:  # the maps of this group beside the next group's model pass
-                    side.wait_stream(main)
-                    with torch.cuda.stream(side):
-                        plan.adjoint_maps(gk, gc, n, c, maps=maps[g0 * n * K:(g0 + gc) * n * K],
-                                          band_max=bmax[g0:g0 + gc])
-                    gk.record_stream(side)
-        if side is not None:
-            main.wait_stream(side)
+                plan.adjoint_maps(gk, gc, n, c, maps=maps[g0 * n * K:(g0 + gc) * n * K], band_max=bmax[g0:g0 + gc])
         last = gk[-n:] if gk.dim() == 4 else gk[-n * c:]
         return maps, bmax, last
 
