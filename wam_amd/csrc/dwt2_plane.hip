@@ -36,6 +36,11 @@ constexpr int kPT = 64 * kPW;          // threads per workgroup
 constexpr int kPlaneMaxW = 256;        // level-0 row width (one float4 per lane)
 constexpr int kPlaneMaxMW = 128;       // level-1 output width (two columns per lane)
 constexpr int kPlaneLdsCap = 160 * 1024 - 1024;
+// waves per workgroup of the noisy wave-chunk analysis (A/B builds: 10 = 5 waves per SIMD at two
+// workgroups per CU, if the kernel fits 96 VGPRs)
+#ifndef WAM_NOISY_PW
+#define WAM_NOISY_PW 8
+#endif
 // noisy wave-chunk level 1 computes the halo rows of the boundaries where a pair of waves meets
 // once (bidirectional chunks); at CPL = 2 lane l filters the ADJACENT columns
 // 2l, 2l+1 (one run of L/2+1 LDS pairs feeds both, each band row stored as float2 pairs)
@@ -170,8 +175,8 @@ struct CoopRow<NCH, kInBf16Nchw> {
 // COOP: level 1 as a cooperative row stream (see phase 1 below) instead of wave-private chunks
 // IN (COOP maps only for the bf16 formats): kInF32, or bf16 images [items, nh, nw, MC] (kInBf16Nhwc)
 // / [items, MC, nh, nw] (kInBf16Nchw)
-template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP, int IN = kInF32>
-__global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))) k_plane_ana(const float* __restrict__ in, float* __restrict__ out,
+template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP, int IN = kInF32, int PW = kPW>
+__global__ void __launch_bounds__(64 * PW) __attribute__((amdgpu_waves_per_eu(PW > 8 ? 5 : 4, 8))) k_plane_ana(const float* __restrict__ in, float* __restrict__ out,
                                                    float* __restrict__ band_max, const float* __restrict__ filt,
                                                    PlaneGeom g, WamNoise nz, int64_t n_items, int64_t S,
                                                    int64_t group_items) {
@@ -211,6 +216,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     sg = nz.sigma[img];
   }
   static_assert(IN == kInF32 || (COOP && MAPS && !NOISE), "bf16 input: COOP maps pass only");
+  static_assert(PW == kPW || (!COOP && NOISE), "other workgroup sizes: noisy wave chunks only");
   const float* src = IN != kInF32 ? reinterpret_cast<const float*>(reinterpret_cast<const uint16_t*>(in) +
                                                                    src_plane * (int64_t)NCH * in_plane)
                                   : in + src_plane * (int64_t)NCH * in_plane;
@@ -272,7 +278,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     const int mode = g.mode;
     const bool zero_mode = mode == WAM_MODE_ZERO;
     float* wrow = bufB + wv * g.rowlds;
-    float2* ring = reinterpret_cast<float2*>(bufB + kPW * g.rowlds);
+    float2* ring = reinterpret_cast<float2*>(bufB + PW * g.rowlds);
     const PadLane pl = pad_lane(lane, nw, p, mode, PADL);
     if (zero_mode && pl.dst >= 0) wrow[pl.dst] = 0.f;
     const int nb = (mh + RB - 1) / RB;
@@ -452,7 +458,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     const bool zero_mode = mode == WAM_MODE_ZERO;
     const PadLane pl = pad_lane(lane, nw, p, mode);
     if (zero_mode && pl.dst >= 0) lds[pl.dst] = 0.f;
-    const int R = (mh + kPW - 1) / kPW;
+    const int R = (mh + PW - 1) / PW;
     const int i0 = wv * R;
     const int i1 = min(mh, i0 + R);
     const int er0 = 2 * i0 - p;
@@ -468,13 +474,13 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     const bool up = SHARE && !(wv & 1);
     const int pw = wv ^ 1;  // partner
     // both waves of the pair have rows, and the LL_1 area (J > 1) holds the exchange
-    const bool share = SHARE && T > 0 && pw * R < mh && g.llcap >= kPW * HS * 2 * CPL * 64;
+    const bool share = SHARE && T > 0 && pw * R < mh && g.llcap >= PW * HS * 2 * CPL * 64;
     // END boundaries (waves 2k-1 top-down | 2k bottom-up) meet at the end of both streams: each
     // computes the first HS of the L - 2 shared rows (its steps T-L+2 .. T-HS-1) and takes the rest
     // from its partner through buffer B (g.xend) after one workgroup barrier. Both waves need
     // >= L - 2 + 2*HS steps so that the START and END shared rows do not overlap.
     const int pe = (wv & 1) ? wv + 1 : wv - 1;
-    const int pe_rows = (pe >= 0 && pe < kPW) ? max(0, min(mh, (pe + 1) * R) - pe * R) : 0;
+    const int pe_rows = (pe >= 0 && pe < PW) ? max(0, min(mh, (pe + 1) * R) - pe * R) : 0;
     const bool end_share = SHARE && g.xend >= 0 && T >= 2 * (L - 2) && 2 * pe_rows + L - 2 >= 2 * (L - 2);
     const int T_stop = end_share ? T - HS : T;  // the loop's last step + 1
     float mx[4] = {0.f, 0.f, 0.f, 0.f};
@@ -752,7 +758,7 @@ __global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(4, 8))
     float mx[4] = {0.f, 0.f, 0.f, 0.f};
     // thread (rb, j): output column j, output rows [i0, i1) of row block rb; a block filters
     // 2R + L - 2 ext rows for R outputs, so blocks are kept >= L rows long where the level allows
-    int nrb = kPT / mw;  // mw <= kPT (geom_ok)
+    int nrb = 64 * PW / mw;  // mw <= kPT (geom_ok)
     if (nrb > max(1, mh / L)) nrb = max(1, mh / L);
     const int rb = tid / mw, j = tid - rb * mw;
     if (rb < nrb) {
@@ -980,7 +986,8 @@ bool coop_ok(const wam_plan* p, int nw0, bool noisy = false) {
   return (int64_t)coop_lds_floats(p, nw0, rowlds, llcap) * 4 <= kTwoWgLds || (p->flags & WAM_PLAN_FORCE_COOP);
 }
 
-int lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap, bool noisy = false, int* xend = nullptr) {
+int lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap, bool noisy = false, int* xend = nullptr,
+               int pw = kPW) {
   if (coop_ok(p, nw0, noisy)) return coop_lds_floats(p, nw0, rowlds, llcap);
   rowlds = kPadL + 256 + 8;  // commit covers 256 samples; pads <= p + 2 <= 20 fit behind them
   if (rowlds < kPadL + nw0 + p->pad + 4) rowlds = kPadL + nw0 + p->pad + 4;
@@ -988,7 +995,7 @@ int lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap, bool noisy =
   // buffer B (the wave rows, read and written with 16-byte ds ops) must start 16-byte aligned: a
   // misaligned b128/b64 LDS access is split by the hardware and made this kernel 3x slower
   llcap = p->levels > 1 ? (int)((p->lout[0][0] * p->lout[0][1] + 63) & ~63) : 0;
-  int64_t bcap = (int64_t)kPW * rowlds;
+  int64_t bcap = (int64_t)pw * rowlds;
   int64_t ll2 = 0;
   if (p->levels > 1) {
     ll2 = p->lout[1][0] * p->lout[1][1];
@@ -998,10 +1005,10 @@ int lds_floats(const wam_plan* p, int nw0, int& rowlds, int& llcap, bool noisy =
   if (noisy) {
     // the END-boundary exchange behind the wave rows: (kPW/2 - 1) boundaries x 2 directions x
     // (L-2)/2 rows x (lo, hi) x mw floats, if two workgroups still fit a CU
-    const int64_t xe = (int64_t)(kPW / 2 - 1) * 2 * (p->L - 2) * p->lout[0][1];
-    const int64_t b2 = std::max<int64_t>((int64_t)kPW * rowlds + xe, ll2);
+    const int64_t xe = (int64_t)(pw / 2 - 1) * 2 * (p->L - 2) * p->lout[0][1];
+    const int64_t b2 = std::max<int64_t>((int64_t)pw * rowlds + xe, ll2);
     if ((llcap + b2) * 4 + 4 * WAM_MAX_BANDS + 64 <= 160 * 1024 / 2) {
-      if (xend) *xend = kPW * rowlds;
+      if (xend) *xend = pw * rowlds;
       bcap = b2;
     }
   }
@@ -1018,7 +1025,8 @@ bool geom_ok(const wam_plan* p, int nw0, int nh0) {
   return (int64_t)lds_floats(p, nw0, rowlds, llcap) * 4 <= kPlaneLdsCap;
 }
 
-PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items_total, bool noisy = false) {
+PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items_total, bool noisy = false,
+                    int pw = kPW) {
   PlaneGeom g{};
   g.J = p->levels;
   g.mode = mode;
@@ -1036,7 +1044,7 @@ PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items
   g.nbands = p->nbands;
   g.items_total = items_total;
   g.maps_item = p->band_off[p->nbands];
-  lds_floats(p, nw0, g.rowlds, g.llcap, noisy, &g.xend);
+  lds_floats(p, nw0, g.rowlds, g.llcap, noisy, &g.xend, pw);
   g.coop = coop_ok(p, nw0, noisy);
   // noisy analysis: sample-fastest through the XCD swizzle (the S samples of a plane read it from
   // one L2; plane-fastest and un-swizzled orders measured 684 / 681 vs 666 us,
@@ -1046,11 +1054,11 @@ PlaneGeom make_geom(const wam_plan* p, int nh0, int nw0, int mode, int64_t items
   return g;
 }
 
-template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP, int IN = kInF32>
+template <int L, int CPL, bool NOISE, int MC, bool MAPS, bool COOP, int IN = kInF32, int PW = kPW>
 int launch_plane_t(const PlaneGeom& g, int lds_bytes, int64_t n_items, const float* in, float* out, float* band_max,
                    const float* filt, const WamNoise& nz, int64_t S, int64_t group_items, const char* name,
                    double bytes, hipStream_t st) {
-  auto kern = k_plane_ana<L, CPL, NOISE, MC, MAPS, COOP, IN>;
+  auto kern = k_plane_ana<L, CPL, NOISE, MC, MAPS, COOP, IN, PW>;
   static std::atomic<uint64_t> attr_set{0};  // opt in to > 64 KB of dynamic LDS, once per device
   int dev = 0;
   WAM_HIP_CHECK(hipGetDevice(&dev));
@@ -1061,7 +1069,7 @@ int launch_plane_t(const PlaneGeom& g, int lds_bytes, int64_t n_items, const flo
     attr_set.fetch_or(bit);
   }
   WamTimer tm(st, name, bytes);
-  hipLaunchKernelGGL(kern, dim3((unsigned)n_items), dim3(kPT), lds_bytes, st, in, out, band_max, filt, g, nz, n_items,
+  hipLaunchKernelGGL(kern, dim3((unsigned)n_items), dim3(64 * PW), lds_bytes, st, in, out, band_max, filt, g, nz, n_items,
                      S, group_items);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
@@ -1129,15 +1137,31 @@ int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in
   const int nw0 = (int)(adjoint ? p->rec_shape[1] : p->lin[0][1]);
   const int mode = adjoint ? WAM_MODE_ZERO : p->mode;
   const float* filt = p->d_filt + (adjoint ? WAM_F_ADJ_LO : WAM_F_ANA_LO) * p->L;
-  const PlaneGeom g = make_geom(p, nh0, nw0, mode, items, nz != nullptr);
+  const int pw = (nz && !coop_ok(p, nw0, true)) ? WAM_NOISY_PW : kPW;
+  const PlaneGeom g = make_geom(p, nh0, nw0, mode, items, nz != nullptr, pw);
   int rowlds, llcap;
-  const int lds_bytes = lds_floats(p, nw0, rowlds, llcap, nz != nullptr) * 4;
+  const int lds_bytes = lds_floats(p, nw0, rowlds, llcap, nz != nullptr, nullptr, pw) * 4;
   const double in_planes = nz ? (double)nz->images * nz->channels : (double)items;
   const double bytes = 4.0 * (in_planes * nh0 * nw0 + (double)items * p->band_off[p->nbands]);
   if (nz) {
     if (items != n_samples * nz->images * nz->channels) return WAM_ERR_INVALID_ARG;
     // the fused noise counts element groups of an image in 32 bits (wam_normal4_x2)
     if ((int64_t)nz->channels * nh0 * nw0 >= (int64_t(1) << 34)) return WAM_ERR_UNSUPPORTED;
+    if (pw != kPW) {
+      if (lds_bytes > 160 * 1024 / 2 - 4 * WAM_MAX_BANDS - 64) return WAM_ERR_UNSUPPORTED;
+      const bool two = g.mw[0] > 64;
+#define WAM_NOISY_CASE(LL)                                                                                       \
+  case LL:                                                                                                       \
+    return two ? launch_plane_t<LL, 2, true, 0, false, false, kInF32, WAM_NOISY_PW>(                            \
+                     g, lds_bytes, items, in, coeffs, nullptr, filt, *nz, n_samples, 1, "k_plane_ana<noise>", bytes, st) \
+               : launch_plane_t<LL, 1, true, 0, false, false, kInF32, WAM_NOISY_PW>(                            \
+                     g, lds_bytes, items, in, coeffs, nullptr, filt, *nz, n_samples, 1, "k_plane_ana<noise>", bytes, st);
+      switch (p->L) {
+        WAM_NOISY_CASE(2) WAM_NOISY_CASE(4) WAM_NOISY_CASE(6) WAM_NOISY_CASE(8)
+        default: return WAM_ERR_UNSUPPORTED;
+      }
+#undef WAM_NOISY_CASE
+    }
     return dispatch_plane<true, 0, false>(p, g, lds_bytes, items, in, coeffs, nullptr, filt, *nz, n_samples, 1,
                                           "k_plane_ana<noise>", bytes, st);
   }
