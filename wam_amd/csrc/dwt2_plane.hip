@@ -36,11 +36,6 @@ constexpr int kPT = 64 * kPW;          // threads per workgroup
 constexpr int kPlaneMaxW = 256;        // level-0 row width (one float4 per lane)
 constexpr int kPlaneMaxMW = 128;       // level-1 output width (two columns per lane)
 constexpr int kPlaneLdsCap = 160 * 1024 - 1024;
-// waves per workgroup of the noisy wave-chunk analysis (A/B builds: 10 = 5 waves per SIMD at two
-// workgroups per CU, if the kernel fits 96 VGPRs)
-#ifndef WAM_NOISY_PW
-#define WAM_NOISY_PW 8
-#endif
 // noisy wave-chunk level 1 computes the halo rows of the boundaries where a pair of waves meets
 // once (bidirectional chunks); at CPL = 2 lane l filters the ADJACENT columns
 // 2l, 2l+1 (one run of L/2+1 LDS pairs feeds both, each band row stored as float2 pairs)
@@ -1137,31 +1132,15 @@ int launch_dwt2_plane_analysis(const wam_plan* p, int64_t items, const float* in
   const int nw0 = (int)(adjoint ? p->rec_shape[1] : p->lin[0][1]);
   const int mode = adjoint ? WAM_MODE_ZERO : p->mode;
   const float* filt = p->d_filt + (adjoint ? WAM_F_ADJ_LO : WAM_F_ANA_LO) * p->L;
-  const int pw = (nz && !coop_ok(p, nw0, true)) ? WAM_NOISY_PW : kPW;
-  const PlaneGeom g = make_geom(p, nh0, nw0, mode, items, nz != nullptr, pw);
+  const PlaneGeom g = make_geom(p, nh0, nw0, mode, items, nz != nullptr);
   int rowlds, llcap;
-  const int lds_bytes = lds_floats(p, nw0, rowlds, llcap, nz != nullptr, nullptr, pw) * 4;
+  const int lds_bytes = lds_floats(p, nw0, rowlds, llcap, nz != nullptr) * 4;
   const double in_planes = nz ? (double)nz->images * nz->channels : (double)items;
   const double bytes = 4.0 * (in_planes * nh0 * nw0 + (double)items * p->band_off[p->nbands]);
   if (nz) {
     if (items != n_samples * nz->images * nz->channels) return WAM_ERR_INVALID_ARG;
     // the fused noise counts element groups of an image in 32 bits (wam_normal4_x2)
     if ((int64_t)nz->channels * nh0 * nw0 >= (int64_t(1) << 34)) return WAM_ERR_UNSUPPORTED;
-    if (pw != kPW) {
-      if (lds_bytes > 160 * 1024 / 2 - 4 * WAM_MAX_BANDS - 64) return WAM_ERR_UNSUPPORTED;
-      const bool two = g.mw[0] > 64;
-#define WAM_NOISY_CASE(LL)                                                                                       \
-  case LL:                                                                                                       \
-    return two ? launch_plane_t<LL, 2, true, 0, false, false, kInF32, WAM_NOISY_PW>(                            \
-                     g, lds_bytes, items, in, coeffs, nullptr, filt, *nz, n_samples, 1, "k_plane_ana<noise>", bytes, st) \
-               : launch_plane_t<LL, 1, true, 0, false, false, kInF32, WAM_NOISY_PW>(                            \
-                     g, lds_bytes, items, in, coeffs, nullptr, filt, *nz, n_samples, 1, "k_plane_ana<noise>", bytes, st);
-      switch (p->L) {
-        WAM_NOISY_CASE(2) WAM_NOISY_CASE(4) WAM_NOISY_CASE(6) WAM_NOISY_CASE(8)
-        default: return WAM_ERR_UNSUPPORTED;
-      }
-#undef WAM_NOISY_CASE
-    }
     return dispatch_plane<true, 0, false>(p, g, lds_bytes, items, in, coeffs, nullptr, filt, *nz, n_samples, 1,
                                           "k_plane_ana<noise>", bytes, st);
   }
