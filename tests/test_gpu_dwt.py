@@ -412,6 +412,46 @@ def test_haar3_blocks_equal_per_axis(wam, shape, J, mode):
     assert torch.equal(fast.adjoint(g), gen.adjoint(g))
 
 
+@pytest.mark.parametrize("wav,shape,J,mode", [("db4", (40, 36, 34), 2, "zero"), ("db2", (17, 23, 30), 2, "reflect"),
+                                              ("sym4", (33, 16, 25), 2, "symmetric"), ("db3", (20, 21, 22), 2, "constant"),
+                                              ("sym8", (48, 40, 36), 2, "reflect"), ("coif1", (19, 18, 17), 1, "periodic"),
+                                              ("haar", (15, 14, 13), 2, "reflect"), ("db6", (64, 64, 64), 2, "symmetric"),
+                                              ("db4", (128, 128, 128), 2, "reflect")])
+def test_dwt3_tile_levels_equal_per_axis(wam, wav, shape, J, mode):
+    """Fused 3D levels (dwt3_tile.hip: the footprint of a tile in LDS, W / H / D passes there, one
+    launch per level) vs the per-axis kernels (three passes per level): wavedec3, waverec3 with IG
+    alphas and the adjoint bit-identical (same axis order, taps and fma chains), odd sizes, every
+    mode, filters of 2-16 taps; the fused kernels must be the ones that ran."""
+    fast = wam.get_plan(3, shape, J, wav, mode, "cuda")
+    gen = wam.get_plan(3, shape, J, wav, mode, "cuda", generic=True)
+    torch.manual_seed(14)
+    B = 2
+    x = torch.randn((B,) + shape, device="cuda")
+    wam.timing_drain()
+    wam.timing_enable(True)
+    a = fast.wavedec(x)
+    torch.cuda.synchronize()
+    wam.timing_enable(False)
+    names = {r[0] for r in wam.timing_drain()}
+    b = gen.wavedec(x)
+    assert torch.equal(a, b)
+    if wav != "haar" or (mode == "reflect" and any(n % 4 for n in shape)):
+        assert "k_dwt3_ana_tile" in names, names
+    al = [0.25, 1.0]
+    wam.timing_drain()
+    wam.timing_enable(True)
+    r = fast.waverec(b, B, alphas=al)
+    torch.cuda.synchronize()
+    wam.timing_enable(False)
+    names = {r_[0] for r_ in wam.timing_drain()}
+    assert torch.equal(r, gen.waverec(b, B, alphas=al))
+    assert torch.equal(fast.waverec(b, B), gen.waverec(b, B))
+    if wav != "haar":
+        assert "k_dwt3_syn_tile" in names, names
+    g = torch.randn((B,) + fast.rec_shape, device="cuda")
+    assert torch.equal(fast.adjoint(g), gen.adjoint(g))
+
+
 @pytest.mark.parametrize("wav,shape,J,mode", [("db4", (224, 224), 3, "reflect"), ("haar", (224, 224), 3, "reflect"),
                                               ("db2", (64, 96), 4, "symmetric"), ("db3", (100, 84), 2, "zero"),
                                               ("db4", (37, 52), 2, "reflect"), ("sym4", (36, 200), 3, "constant"),

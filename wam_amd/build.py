@@ -21,7 +21,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libwam_hip.so")
 OBJ_CACHE = os.path.join(os.path.dirname(HERE), "build", "obj")
 SOURCES = ["plan.hip", "dwt_axis.hip", "dwt2_fused.hip", "dwt2_rows.hip", "dwt2_plane.hip",
-           "dwt1_tile.hip", "dwt3_haar.hip", "epilogue.hip", "evaluate.hip", "visualize3d.hip", "melspec.hip",
+           "dwt1_tile.hip", "dwt3_haar.hip", "dwt3_tile.hip", "epilogue.hip", "evaluate.hip", "visualize3d.hip", "melspec.hip",
            "model_ew.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("WAM_OFFLOAD_ARCH", "gfx950")

@@ -75,6 +75,14 @@ bool dwt2_plane_syn_supported(const wam_plan* p);
 int launch_dwt2_plane_synthesis(const wam_plan* p, int64_t batch, const float* coeffs, const float* alpha,
                                 int n_alpha, void* out, int out_channels, hipStream_t st);
 
+// fused 3D levels, any even filter up to 16 taps (dwt3_tile.hip): one launch per level
+bool dwt3_tile_supported(const wam_plan* p);
+int launch_dwt3_analysis_tile(const wam_plan* p, int64_t batch, const float* in, const int64_t* in_dims,
+                              const int64_t* out_dims, int mode, int fset, float* out_a, float* const* sub,
+                              hipStream_t st);
+int launch_dwt3_synthesis_tile(const wam_plan* p, int64_t batch, int level, const float* a_in, float a_scale,
+                               const float* const* sub, float d_scale, float* out, hipStream_t st);
+
 // fused multi-level 1D tiles (dwt1_tile.hip)
 bool dwt1_tile_supported(const wam_plan* p, bool adjoint);
 

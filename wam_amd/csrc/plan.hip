@@ -433,7 +433,11 @@ int analysis_driver(const wam_plan* p, int64_t batch, const float* x, float* coe
     } else if (use_colstrip(p)) {
       rc = launch_dwt2_analysis_fused(p, batch, cur, in_dims, p->lout[l], mode, fset, out_a, sub, st);
     } else {
-      rc = generic_analysis_level(p, batch, cur, in_dims, p->lout[l], mode, fset, out_a, sub, tmp, st);
+      rc = WAM_ERR_UNSUPPORTED;
+      if (p->ndim == 3 && dwt3_tile_supported(p))  // all three axes of the level in one pass
+        rc = launch_dwt3_analysis_tile(p, batch, cur, in_dims, p->lout[l], mode, fset, out_a, sub, st);
+      if (rc == WAM_ERR_UNSUPPORTED)
+        rc = generic_analysis_level(p, batch, cur, in_dims, p->lout[l], mode, fset, out_a, sub, tmp, st);
     }
     if (rc) return rc;
     cur = out_a;
@@ -617,7 +621,10 @@ int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const flo
       float* sub[7];
       band_ptrs(p, batch, (float*)coeffs, l, sub);
       float* dst = (l == 0) ? out + (int64_t)ai * batch * out_item : abuf[c & 1];
-      int rc = generic_synthesis_level(p, batch, l, a_cur, a_scale, sub, s, dst, tmp, st);
+      int rc = WAM_ERR_UNSUPPORTED;
+      if (nd == 3 && dwt3_tile_supported(p))  // all three axes of the level in one pass
+        rc = launch_dwt3_synthesis_tile(p, batch, l, a_cur, a_scale, sub, s, dst, st);
+      if (rc == WAM_ERR_UNSUPPORTED) rc = generic_synthesis_level(p, batch, l, a_cur, a_scale, sub, s, dst, tmp, st);
       if (rc) return rc;
       a_cur = dst;
       a_scale = 1.0f;
