@@ -419,9 +419,10 @@ def test_haar3_blocks_equal_per_axis(wam, shape, J, mode):
                                               ("db4", (128, 128, 128), 2, "reflect")])
 def test_dwt3_tile_levels_equal_per_axis(wam, wav, shape, J, mode):
     """Fused 3D levels (dwt3_tile.hip: the footprint of a tile in LDS, W / H / D passes there, one
-    launch per level) vs the per-axis kernels (three passes per level): wavedec3, waverec3 with IG
-    alphas and the adjoint bit-identical (same axis order, taps and fma chains), odd sizes, every
-    mode, filters of 2-16 taps; the fused kernels must be the ones that ran."""
+    launch per level; filters up to 8 taps) vs the per-axis kernels (three passes per level):
+    wavedec3, waverec3 with IG alphas and the adjoint bit-identical (same axis order, taps and fma
+    chains), odd sizes, every mode; the fused kernels must be the ones that ran (db6 / sym8 keep the
+    per-axis path and are checked as a regression)."""
     fast = wam.get_plan(3, shape, J, wav, mode, "cuda")
     gen = wam.get_plan(3, shape, J, wav, mode, "cuda", generic=True)
     torch.manual_seed(14)
@@ -435,7 +436,9 @@ def test_dwt3_tile_levels_equal_per_axis(wam, wav, shape, J, mode):
     names = {r[0] for r in wam.timing_drain()}
     b = gen.wavedec(x)
     assert torch.equal(a, b)
-    if wav != "haar" or (mode == "reflect" and any(n % 4 for n in shape)):
+    from wam_amd.filters import get_wavelet
+    fused = len(get_wavelet(wav).dec_lo) <= 8  # longer filters keep the per-axis kernels
+    if fused and (wav != "haar" or any(n % 4 for n in shape)):
         assert "k_dwt3_ana_tile" in names, names
     al = [0.25, 1.0]
     wam.timing_drain()
@@ -446,7 +449,7 @@ def test_dwt3_tile_levels_equal_per_axis(wam, wav, shape, J, mode):
     names = {r_[0] for r_ in wam.timing_drain()}
     assert torch.equal(r, gen.waverec(b, B, alphas=al))
     assert torch.equal(fast.waverec(b, B), gen.waverec(b, B))
-    if wav != "haar":
+    if fused and wav != "haar":
         assert "k_dwt3_syn_tile" in names, names
     g = torch.randn((B,) + fast.rec_shape, device="cuda")
     assert torch.equal(fast.adjoint(g), gen.adjoint(g))
