@@ -25,9 +25,13 @@ int launch_dwt2_analysis_fused(const wam_plan* p, int64_t batch, const float* in
                                hipStream_t st);
 // One synthesis level for up to kSynMaxAlpha IG alphas in one launch: alpha i reads its LL from
 // a[i] (scaled by sa[i]) and the shared detail bands (scaled by sd[i]) and writes out[i].
-constexpr int kSynMaxAlpha = 8;
+constexpr int kSynMaxAlpha = 32;
 // alphas whose intermediate LL planes the plan workspace holds at once (2D row-synthesis plans)
-constexpr int kSynWsAlpha = 8;
+#ifndef WAM_SYN_WS_ALPHA
+#define WAM_SYN_WS_ALPHA 8
+#endif
+constexpr int kSynWsAlpha = WAM_SYN_WS_ALPHA;
+static_assert(kSynWsAlpha >= 1 && kSynWsAlpha <= kSynMaxAlpha, "alpha group");
 struct SynBatch {
   const float* a[kSynMaxAlpha];
   float* out[kSynMaxAlpha];

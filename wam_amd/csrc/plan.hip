@@ -588,8 +588,8 @@ int wam_waverec(const wam_plan* p, int64_t batch, const float* coeffs, const flo
     // alphas in groups: one launch per level per group, each level's detail bands read once per
     // group; the group's intermediate LL planes ping-pong between two workspace sets
     const int64_t ws_elems = wam_plan_workspace_bytes(p, batch) / (int64_t)sizeof(float) - 64;
-    int64_t g = rec_ll > 0 ? ws_elems / (2 * rec_ll) : kSynMaxAlpha;
-    const int G = (int)(g < 1 ? 1 : (g > kSynMaxAlpha ? kSynMaxAlpha : g));
+    int64_t g = rec_ll > 0 ? ws_elems / (2 * rec_ll) : kSynWsAlpha;
+    const int G = (int)(g < 1 ? 1 : (g > kSynWsAlpha ? kSynWsAlpha : g));
     for (int a0 = 0; a0 < n_alpha; a0 += G) {
       SynBatch sb{};
       sb.na = n_alpha - a0 < G ? n_alpha - a0 : G;
