@@ -268,8 +268,8 @@ __global__ void __launch_bounds__(kT3) k_haar3_syn(const float* __restrict__ coe
 #pragma unroll
     for (int y = 0; y < B; ++y) {
       float* row = dst + ((int64_t)z * g.H + y) * g.W;
-      if constexpr (B == 4) *reinterpret_cast<float4*>(row) = make_float4(v[z][y][0], v[z][y][1], v[z][y][2], v[z][y][3]);
-      else *reinterpret_cast<float2*>(row) = make_float2(v[z][y][0], v[z][y][1]);
+      if constexpr (B == 4) wam_st4(row, v[z][y][0], v[z][y][1], v[z][y][2], v[z][y][3]);
+      else wam_st(reinterpret_cast<wam_f2v*>(row), wam_f2v{v[z][y][0], v[z][y][1]});
     }
 }
 

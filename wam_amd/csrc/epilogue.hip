@@ -701,7 +701,7 @@ __global__ void __launch_bounds__(256) k_disentangle(int64_t items, int size, in
 typedef float wam_f4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(256) k_copy(int64_t n4, const wam_f4* __restrict__ src, wam_f4* __restrict__ dst) {
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += step) dst[t] = src[t];
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += step) wam_st(dst + t, src[t]);
 }
 
 }  // namespace

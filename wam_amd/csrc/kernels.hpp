@@ -11,6 +11,33 @@ __device__ __forceinline__ int64_t wam_xcd_block(int64_t bid, int64_t nwg) {
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
 }
 
+// Streaming stores (global_store ... nt): same bytes, same values, no write-allocation in the caches.
+// Used where they won in the bench's own pipeline: the 3D Haar synthesis, whose output is the model's
+// input and read by no WAM kernel (c5 in-bench, profiles/r06y_*: k_haar3_syn 103 -> 87 us per launch,
+// WAM 4.88 -> 4.65 ms per step), and k_copy (the copy ceiling 6.18 -> 6.32 TB/s,
+// r06w_ab_copy_nt.log). Back-to-back microbenchmarks flatter them -- there plain stores pay the
+// previous launch's write-back (c5 maps 110 -> 83 us in kbench, 111 -> 100-118 in the pipeline,
+// r06t_* / r06x_*) -- and elsewhere they measured the same or slower: c4's finest synthesis level
+// (r06y_*), the plane / row / 1D / mel kernels (noisy plane analysis 606-641 -> 644-667 us; the bf16
+// NHWC synthesis's 2-byte stores 496 -> 1,070 us; r06u_*, r06v_*). WAM_NT_STORES=0 builds the plain
+// stores for A/B runs.
+#ifndef WAM_NT_STORES
+#define WAM_NT_STORES 1
+#endif
+typedef float wam_f2v __attribute__((ext_vector_type(2)));  // 8-byte aligned pair
+typedef float wam_f4v __attribute__((ext_vector_type(4)));
+template <class T>
+__device__ __forceinline__ void wam_st(T* p, T v) {
+#if WAM_NT_STORES
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ void wam_st4(float* p, float a, float b, float c, float d) {  // 16-byte aligned
+  wam_st(reinterpret_cast<wam_f4v*>(p), wam_f4v{a, b, c, d});
+}
+
 // generic per-axis kernels (dwt_axis.hip)
 int launch_analysis_axis(const float* in, float* lo, float* hi, int64_t outer, int n, int m, int64_t inner,
                          int padl, int mode, const float* flo, const float* fhi, int L, hipStream_t st);
