@@ -61,3 +61,41 @@ def test_trapz_coef_order_equals_gather(shape, wav, J, normalize, weighted):
     torch.cuda.synchronize()
     assert torch.equal(acc_a, acc_b) and torch.equal(prev_a, prev_b)
     assert acc_a.abs().sum() > 0
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("groups", [1, 2, 5])
+@pytest.mark.parametrize("cube", [4 * 3072, 4 * 3000])  # 3 x cube % 256 == 0: the strided form; else 4 consecutive
+def test_cube_accumulate_vec4_equals_scalar(mode, groups, cube):
+    """wam_cube_accumulate's four-voxel forms (16-byte aligned index / accumulator, cube_len % 4 == 0;
+    strided over 256-voxel wave blocks when the work divides, the c5 path) vs its one-voxel form (the
+    same index map handed over misaligned): bit-identical acc and prev in every mode -- legacy in-loop
+    averaging, weighted sum, trapezoid over two chained passes with NaN / inf map values -- with
+    voxels outside the mosaic (index -1) included."""
+    from wam_amd import plan as P
+    torch.manual_seed(7 + mode + groups + cube)
+    n, items_len = 3, cube + 64
+    src = torch.randperm(items_len, device="cuda")[:cube].to(torch.int32)
+    src[::13] = -1
+    buf = torch.empty(cube + 1, dtype=torch.int32, device="cuda")
+    buf[1:] = src
+    src_mis = buf[1:]  # 4-byte offset: the one-voxel kernel
+    assert src.data_ptr() % 16 == 0 and src_mis.data_ptr() % 16 != 0
+    acc_a = torch.rand(n * cube, device="cuda")
+    prev_a = torch.rand(n * cube, device="cuda") if mode == 2 else None
+    acc_b = acc_a.clone()
+    prev_b = prev_a.clone() if prev_a is not None else None
+    k0 = 0
+    for _ in range(2):
+        maps = torch.randn(groups * n * items_len, device="cuda")
+        if mode == 2:
+            maps[::997] = float("nan")
+            maps[5::1999] = float("inf")
+        w = torch.rand(groups, device="cuda") if mode == 1 else None
+        P.cube_accumulate(groups, k0, n, src, maps, items_len, mode, 25.0, acc_a, prev=prev_a, weights=w)
+        P.cube_accumulate(groups, k0, n, src_mis, maps, items_len, mode, 25.0, acc_b, prev=prev_b, weights=w)
+        k0 += groups
+    torch.cuda.synchronize()
+    assert torch.equal(acc_a, acc_b)
+    if mode == 2:
+        assert torch.equal(prev_a, prev_b)

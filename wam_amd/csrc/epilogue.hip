@@ -539,6 +539,86 @@ __global__ void __launch_bounds__(256) k_cube_accumulate(int64_t groups, int64_t
   }
 }
 
+// the same, four voxels per thread, all index / accumulator / gathered map loads of a thread issued
+// before the first use -- the one-voxel form made every voxel a dependent index -> map load chain
+// (c5: 178 us per launch, profiles/r06z_trace_window_c5.txt). Per voxel the sample order and the
+// arithmetic are unchanged. STRIDED: voxels b + lane + 64 u (u < 4) of a 256-voxel wave block, so
+// each load instruction covers 64 consecutive voxels (the gathers follow the mosaic's runs of
+// consecutive coefficients); otherwise four consecutive voxels per thread with 16-byte index /
+// accumulator accesses (cube_len % 4 == 0, 16-byte aligned).
+template <bool STRIDED>
+__global__ void __launch_bounds__(256) k_cube_accumulate4(int64_t groups, int64_t k0, int64_t group_items,
+                                                          int64_t cube_len, const int32_t* __restrict__ src,
+                                                          const float* __restrict__ maps, int64_t maps_item_len,
+                                                          int mode, float n_total, const float* __restrict__ weights,
+                                                          float* __restrict__ prev, float* __restrict__ acc) {
+  const int64_t total4 = group_items * cube_len / 4;  // 4-voxel units (cube_len % 4 == 0)
+  const int lane = threadIdx.x & 63;
+  for (int64_t t4 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t4 < total4; t4 += (int64_t)gridDim.x * blockDim.x) {
+    int64_t tv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tv[e] = STRIDED ? 4 * (t4 - lane) + lane + 64 * e : 4 * t4 + e;
+    int sv[4];
+    float a[4], pv[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (STRIDED) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sv[e] = src[tv[e] % cube_len];
+        a[e] = acc[tv[e]];
+        if (prev) pv[e] = prev[tv[e]];
+      }
+    } else {
+      const int4 si = *reinterpret_cast<const int4*>(src + tv[0] % cube_len);
+      sv[0] = si.x, sv[1] = si.y, sv[2] = si.z, sv[3] = si.w;
+      const float4 a4 = *reinterpret_cast<const float4*>(acc + tv[0]);
+      a[0] = a4.x, a[1] = a4.y, a[2] = a4.z, a[3] = a4.w;
+      if (prev) {
+        const float4 p4 = *reinterpret_cast<const float4*>(prev + tv[0]);
+        pv[0] = p4.x, pv[1] = p4.y, pv[2] = p4.z, pv[3] = p4.w;
+      }
+    }
+    int64_t nv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) nv[e] = tv[e] / cube_len;
+    for (int64_t s = 0; s < groups; s += 4) {  // up to 4 samples' gathers in flight per voxel
+      float v[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t su = s + u < groups ? s + u : s;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[u][e] = maps[(su * group_items + nv[e]) * maps_item_len + (sv[e] >= 0 ? sv[e] : 0)];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (s + u >= groups) break;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = sv[e] >= 0 ? v[u][e] : 0.f;
+          if (mode == 0) {
+            a[e] = (a[e] + x) / n_total;
+          } else if (mode == 1) {
+            a[e] = fmaf(weights[s + u], x, a[e]);
+          } else {
+            x = nan_to_num(x);
+            if (k0 + s + u > 0) a[e] = a[e] + (pv[e] + x) / 2.0f;
+            pv[e] = x;
+          }
+        }
+      }
+    }
+    if constexpr (STRIDED) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[tv[e]] = a[e];
+        if (prev) prev[tv[e]] = pv[e];
+      }
+    } else {
+      *reinterpret_cast<float4*>(acc + tv[0]) = make_float4(a[0], a[1], a[2], a[3]);
+      if (prev) *reinterpret_cast<float4*>(prev + tv[0]) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) k_accumulate_f32(int64_t groups, int64_t len, const float* __restrict__ src,
                                                         float scale, float* __restrict__ acc) {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < len; e += (int64_t)gridDim.x * blockDim.x) {
@@ -903,8 +983,23 @@ int wam_cube_accumulate(int64_t groups, int64_t k0, int64_t group_items, int64_t
   if ((mode == 1 && !weights) || (mode == 2 && !prev)) return WAM_ERR_INVALID_ARG;
   int64_t work = group_items * cube_len;
   if (work == 0 || groups == 0) return WAM_OK;
-  hipLaunchKernelGGL(k_cube_accumulate, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, groups, k0,
-                     group_items, cube_len, src, maps, maps_item_len, mode, n_total, weights, prev, acc);
+  // algorithmic bytes: the gathered maps once per (sample, voxel), the accumulator (and trapezoid
+  // state) read and written, the index map once
+  WamTimer tm((hipStream_t)stream, "k_cube_accumulate",
+              4.0 * (double)groups * work + (mode == 2 ? 16.0 : 8.0) * work + 4.0 * cube_len);
+  const bool vec4 = cube_len % 4 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)acc & 15) == 0 &&
+                    ((uintptr_t)prev & 15) == 0;
+  // strided (256-voxel wave blocks, work % 256 == 0): c5 154 -> 109 us per launch against the four
+  // consecutive voxels per thread (profiles/r06zb_ab_cube_accumulate.log)
+  if (vec4 && work % 256 == 0)
+    hipLaunchKernelGGL(k_cube_accumulate4<true>, dim3(wam_grid(work / 4, 256)), dim3(256), 0, (hipStream_t)stream, groups,
+                       k0, group_items, cube_len, src, maps, maps_item_len, mode, n_total, weights, prev, acc);
+  else if (vec4)
+    hipLaunchKernelGGL(k_cube_accumulate4<false>, dim3(wam_grid(work / 4, 256)), dim3(256), 0, (hipStream_t)stream,
+                       groups, k0, group_items, cube_len, src, maps, maps_item_len, mode, n_total, weights, prev, acc);
+  else
+    hipLaunchKernelGGL(k_cube_accumulate, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, groups, k0,
+                       group_items, cube_len, src, maps, maps_item_len, mode, n_total, weights, prev, acc);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }
