@@ -666,49 +666,64 @@ __global__ void __launch_bounds__(256) k_trapz_f32(int64_t groups, int64_t k0, i
 
 // ------------------------------------------------------------------------------ .scales
 // cv2.resize INTER_LINEAR (upsampling): src = (dst + 0.5) * (in / out) - 0.5, clamped to the edge.
-__device__ __forceinline__ double bilinear(const double* __restrict__ img, int ld, int ih, int iw, int oy, int ox,
-                                           int out) {
-  double sy = ((double)oy + 0.5) * ((double)ih / out) - 0.5;
-  double sx = ((double)ox + 0.5) * ((double)iw / out) - 0.5;
-  if (sy < 0) sy = 0;
-  if (sx < 0) sx = 0;
-  int y0 = (int)sy, x0 = (int)sx;
-  if (y0 > ih - 1) y0 = ih - 1;
-  if (x0 > iw - 1) x0 = iw - 1;
-  int y1 = y0 + (y0 < ih - 1 ? 1 : 0), x1 = x0 + (x0 < iw - 1 ? 1 : 0);
-  double fy = sy - y0, fx = sx - x0;
-  if (fy > 1) fy = 1;
-  if (fx > 1) fx = 1;
-  double v00 = img[(int64_t)y0 * ld + x0], v01 = img[(int64_t)y0 * ld + x1];
-  double v10 = img[(int64_t)y1 * ld + x0], v11 = img[(int64_t)y1 * ld + x1];
+// r = (double)in / out is computed on the host once per level (the same IEEE quotient the kernel formed
+// per output before). One axis: source taps i0, i1 and the weight f of output coordinate o.
+struct LinAxis {
+  int i0, i1;
+  double f;
+};
+__device__ __forceinline__ LinAxis lin_axis(int o, double r, int n_in) {
+  double sv = ((double)o + 0.5) * r - 0.5;
+  if (sv < 0) sv = 0;
+  int i0 = (int)sv;
+  if (i0 > n_in - 1) i0 = n_in - 1;
+  const int i1 = i0 + (i0 < n_in - 1 ? 1 : 0);
+  double f = sv - i0;
+  if (f > 1) f = 1;
+  return {i0, i1, f};
+}
+__device__ __forceinline__ double bilinear(const double* __restrict__ img, int ld, const LinAxis& y, const LinAxis& x) {
+  const double fy = y.f, fx = x.f;
+  double v00 = img[(int64_t)y.i0 * ld + x.i0], v01 = img[(int64_t)y.i0 * ld + x.i1];
+  double v10 = img[(int64_t)y.i1 * ld + x.i0], v11 = img[(int64_t)y.i1 * ld + x.i1];
   return (1 - fy) * ((1 - fx) * v00 + fx * v01) + fy * ((1 - fx) * v10 + fx * v11);
 }
 
-__global__ void __launch_bounds__(256) k_reproject(int64_t items, int size, int levels, int approx,
+// per level j (finest first): the quadrant split s = size / 2^(j+1), n = size / 2^j - s and the
+// resize ratios s / size, n / size; the approximation (j = levels): e = size / 2^levels
+struct ReprojGeom {
+  int s[WAM_MAX_LEVELS + 1], n[WAM_MAX_LEVELS + 1];
+  double rs[WAM_MAX_LEVELS + 1], rn[WAM_MAX_LEVELS + 1];
+};
+
+// grid: y = output plane (item, level) -- its index split once per workgroup, x = pixels with 32-bit
+// row / column arithmetic (the flat 64-bit t -> (item, level, y, x) split cost three emulated 64-bit
+// divisions per output: c4 1.41 ms per call)
+__global__ void __launch_bounds__(256) k_reproject(int64_t items, int size, int levels, int approx, ReprojGeom g,
                                                    const double* __restrict__ avg, double* __restrict__ out) {
   const int nl = levels + (approx ? 1 : 0);
-  const int64_t plane = (int64_t)size * size;
-  const int64_t total = items * nl * plane;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    int64_t pix = t % plane;
-    int64_t q = t / plane;
-    int j = (int)(q % nl);
-    int64_t it = q / nl;
-    int oy = (int)(pix / size), ox = (int)(pix % size);
-    const double* a = avg + it * plane;
-    double v;
-    if (j < levels) {
-      int e = (int)(size / (double)(1 << j));
-      int s = (int)(size / (double)(1 << (j + 1)));
-      int n = e - s;
-      // horizontal = avg[:s, s:e], vertical = avg[s:e, :s], diagonal = avg[s:e, s:e]
-      v = bilinear(a + s, size, s, n, oy, ox, size) + bilinear(a + (int64_t)s * size, size, n, s, oy, ox, size) +
-          bilinear(a + (int64_t)s * size + s, size, n, n, oy, ox, size);
-    } else {
-      int e = (int)(size / (double)(1 << levels));
-      v = bilinear(a, size, e, e, oy, ox, size);
+  const unsigned plane = (unsigned)size * (unsigned)size;
+  for (int64_t q = blockIdx.y; q < items * nl; q += gridDim.y) {
+    const int j = (int)(q % nl);
+    const double* a = avg + (q / nl) * (int64_t)plane;
+    double* o = out + q * (int64_t)plane;
+    for (unsigned pix = blockIdx.x * 256u + threadIdx.x; pix < plane; pix += gridDim.x * 256u) {
+      const int oy = (int)(pix / (unsigned)size), ox = (int)(pix - (unsigned)oy * (unsigned)size);
+      double v;
+      if (j < levels) {
+        const int s = g.s[j], n = g.n[j];
+        // the three quadrants share two row and two column interpolations
+        const LinAxis ys = lin_axis(oy, g.rs[j], s), yn = lin_axis(oy, g.rn[j], n);
+        const LinAxis xs = lin_axis(ox, g.rs[j], s), xn = lin_axis(ox, g.rn[j], n);
+        // horizontal = avg[:s, s:e], vertical = avg[s:e, :s], diagonal = avg[s:e, s:e]
+        v = bilinear(a + s, size, ys, xn) + bilinear(a + (int64_t)s * size, size, yn, xs) +
+            bilinear(a + (int64_t)s * size + s, size, yn, xn);
+      } else {
+        const int e = g.n[levels];
+        v = bilinear(a, size, lin_axis(oy, g.rn[levels], e), lin_axis(ox, g.rn[levels], e));
+      }
+      o[pix] = v;
     }
-    out[t] = v;
   }
 }
 
@@ -1028,10 +1043,25 @@ int wam_trapz_f32(int64_t groups, int64_t k0, int64_t len, const float* src, con
 int wam_reproject_scales(int64_t items, int size, int levels, int approx, const double* avg, double* out,
                          void* stream) {
   if (items < 0 || size < 1 || levels < 1 || !avg || !out) return WAM_ERR_INVALID_ARG;
+  if (levels > WAM_MAX_LEVELS) return WAM_ERR_UNSUPPORTED;
   int64_t work = items * (levels + (approx ? 1 : 0)) * (int64_t)size * size;
   if (work == 0) return WAM_OK;
-  hipLaunchKernelGGL(k_reproject, dim3(wam_grid(work, 256)), dim3(256), 0, (hipStream_t)stream, items, size, levels,
-                     approx, avg, out);
+  ReprojGeom g{};
+  for (int j = 0; j < levels; ++j) {  // the reference's int(size / 2**j) splits (lib/wam_2D.py:488-536)
+    const int e = (int)(size / (double)(1 << j)), s = (int)(size / (double)(1 << (j + 1)));
+    g.s[j] = s;
+    g.n[j] = e - s;
+    g.rs[j] = (double)s / size;
+    g.rn[j] = (double)(e - s) / size;
+  }
+  g.n[levels] = (int)(size / (double)(1 << levels));
+  g.rn[levels] = (double)g.n[levels] / size;
+  // algorithmic bytes: every output written once, the averaged map read once
+  WamTimer tm((hipStream_t)stream, "k_reproject", 8.0 * (double)work + 8.0 * (double)items * size * size);
+  if ((int64_t)size * size >= (int64_t(1) << 32)) return WAM_ERR_UNSUPPORTED;  // 32-bit pixel index
+  const int64_t planes = items * (levels + (approx ? 1 : 0));
+  const dim3 grid(wam_grid((int64_t)size * size, 256, 4096), (unsigned)(planes < 65535 ? planes : 65535));
+  hipLaunchKernelGGL(k_reproject, grid, dim3(256), 0, (hipStream_t)stream, items, size, levels, approx, g, avg, out);
   WAM_LAUNCH_CHECK();
   return WAM_OK;
 }
