@@ -1022,6 +1022,7 @@ int wam_cube_accumulate(int64_t groups, int64_t k0, int64_t group_items, int64_t
 int wam_accumulate_f32(int64_t groups, int64_t len, const float* src, float scale, float* acc, void* stream) {
   if (groups < 0 || len < 0 || !src || !acc) return WAM_ERR_INVALID_ARG;
   if (len == 0) return WAM_OK;
+  WamTimer tm((hipStream_t)stream, "k_accumulate_f32", 4.0 * (double)groups * len + 8.0 * (double)len);
   hipLaunchKernelGGL(k_accumulate_f32, dim3(wam_grid(len, 256)), dim3(256), 0, (hipStream_t)stream, groups, len, src,
                      scale, acc);
   WAM_LAUNCH_CHECK();
@@ -1034,6 +1035,8 @@ int wam_trapz_f32(int64_t groups, int64_t k0, int64_t len, const float* src, con
   if (!acc_f64 && !acc_f32) return WAM_ERR_INVALID_ARG;
   if (!weights && !(acc_f64 ? (void*)prev_f64 : (void*)prev_f32)) return WAM_ERR_INVALID_ARG;
   if (len == 0 || groups == 0) return WAM_OK;
+  WamTimer tm((hipStream_t)stream, "k_trapz_f32",
+              4.0 * (double)groups * len + (acc_f64 ? 16.0 : 8.0) * (double)len * (weights ? 1.0 : 2.0));
   hipLaunchKernelGGL(k_trapz_f32, dim3(wam_grid(len, 256)), dim3(256), 0, (hipStream_t)stream, groups, k0, len, src,
                      weights, prev_f32, acc_f32, prev_f64, acc_f64);
   WAM_LAUNCH_CHECK();
