@@ -29,6 +29,8 @@ def short(name):
         return "k_plane_ana<noise>" if args[2] == "true" else "k_plane_ana"
     if base == "k_plane_syn" and len(args) >= 2 and args[1] != "0":  # <L, OC>: bf16 NHWC output
         return "k_plane_syn<bf16nhwc>"
+    if base == "k_cube_accumulate4":  # the four-voxel forms time under the entry point's name
+        return "k_cube_accumulate"
     return base
 
 
