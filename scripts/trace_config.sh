@@ -17,6 +17,7 @@ KT=$(find /tmp/trace_$CFG -name "*kernel_trace.csv" | head -1)
 KS=$(find /tmp/trace_$CFG -name "*kernel_stats.csv" | head -1)
 [ -n "$KS" ] && cp "$KS" $O/kernel_stats.csv
 [ -n "$KT" ] && python3 $R/scripts/trace_window.py "$KT" $WIN $O/kernel_stats_window.csv > $O/window.txt
+[ -n "$KT" ] && python3 $R/scripts/trace_gaps.py "$KT" $WIN > $O/gaps.txt
 rm -rf /tmp/trace_$CFG
 tail -3 $O/bench.log
 exit $rc
